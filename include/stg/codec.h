@@ -1,0 +1,132 @@
+/*
+ * stg/codec.h -- C-ABI of the MI355X-native StellaTrain gradient codec.
+ *
+ * This is the drop-in boundary.  It replaces the reference's
+ *   class Compressor { virtual size_t compress(const std::string &name,
+ *       ConstSegment<float> src, uint32_t k, Segment<uint32_t> dst_idx,
+ *       Segment<float> dst_val, int32_t idx_offset = 0) = 0; }
+ * (/root/reference/backend/src/compress/compressor.h:12-31) and its three
+ * factory-selected implementations (engine/core.cpp:110-118, 185-195):
+ *   "thresholdv16" -> ThresholdvCompressor16  (compress/thresholdv16.h:9-38)
+ *   "thresholdv"   -> ThresholdvCompressor    (compress/thresholdv.h:9-29)
+ *   "topk"         -> TopkCompressor          (compress/topk.h:9-31)
+ * plus the inverse path of config 5: the MERGE decompress
+ * (engine/modules/cpu_optimize.cpp:40-72) and the sparse SGD apply
+ * (optim/sgd.cpp:34-263, SparseOptimizer::optimize_raw sparse_optimizer.h:42).
+ *
+ * Plain pointers and sizes only; no C++ or torch types cross this boundary.
+ * Every entry point returns an int status (STG_OK == 0, < 0 on error) and
+ * never throws; stg_last_error() returns a thread-local message.  The C++
+ * shim in stg/compressor.h turns errors back into std::runtime_error, which
+ * is what the reference throws (topk.cpp:34, core.cpp:117,193).
+ *
+ * Device pointers are HIP device (or host-mapped) pointers on the handle's
+ * device; `stream` is a hipStream_t passed as void* (NULL = legacy default
+ * stream).  Device entry points are asynchronous and never synchronise the
+ * host; host entry points copy in, run, copy out and synchronise.
+ */
+#ifndef STG_CODEC_H
+#define STG_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STG_OK 0
+#define STG_ERR_INVALID (-1)     /* bad argument (e.g. capacity < k for topk)   */
+#define STG_ERR_UNKNOWN (-2)     /* unknown method string                       */
+#define STG_ERR_HIP (-3)         /* HIP runtime error                           */
+#define STG_ERR_UNSUPPORTED (-4) /* size outside what this build handles        */
+#define STG_ERR_DEVICE (-5)      /* device-side failure flag (see stg_check)    */
+
+typedef struct stg_codec *stg_codec_t;
+typedef struct stg_sgd *stg_sgd_t;
+
+/* Method strings as in the reference factory (core.cpp:110-118).
+ * "topk" reproduces the reference's shipped behaviour (the byte-count memcpy
+ * of topk.cpp:31 and idx = 0..k-1); "topk_exact" is the intended top-k by
+ * |x| over the whole bucket with real indices.  Replaces the
+ * ThresholdvCompressor16 / ThresholdvCompressor / TopkCompressor
+ * constructors (thresholdv16.h:33, thresholdv.h:25, topk.h:28). */
+int stg_codec_create(const char *method, int device, stg_codec_t *out);
+int stg_codec_destroy(stg_codec_t h);
+/* Compressor::name() (compressor.h:28): "Thresholdv16", "Thresholdv", "Topk". */
+const char *stg_codec_name(stg_codec_t h);
+
+/* Compressor::compress on host memory (compressor.h:30), the engine's MERGE
+ * call site (engine/modules/compress.cpp:141) and FasterDpEngine::compress
+ * (core.cpp:1210-1245).  Copies src to the device, runs the codec, copies
+ * (idx, val) back and synchronises.  *out_count receives compress()'s return
+ * value.  `key` is the reference's `name` argument (persistent key
+ * "layer@param", task.cpp:56-61); threshold-v ignores it and keys its AIMD
+ * state by the src pointer value, as thresholdv.cpp:44 does. */
+int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, size_t n, uint32_t k,
+                            uint32_t *dst_idx, size_t idx_cap, float *dst_val, size_t val_cap,
+                            int32_t idx_offset, size_t *out_count);
+
+/* Same contract on device-resident buffers, fully asynchronous on `stream`:
+ * no host synchronisation, per-key threshold state stays on the device.
+ * The returned pair count is written to *d_count (device uint32).  dst
+ * buffers are caller-owned with capacity idx_cap (val_cap >= idx_cap). */
+int stg_codec_compress_device(stg_codec_t h, const char *key, const float *d_src, size_t n, uint32_t k,
+                              uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap,
+                              int32_t idx_offset, uint32_t *d_count, void *stream);
+
+/* Per-key AIMD state (thresholdv16.cpp:243-259, thresholdv.cpp:72-80), read
+ * back for parity tests; synchronises `stream`.  Returns STG_ERR_INVALID when
+ * the key has never been compressed.  For threshold-v pass the src pointer
+ * value as `key_ptr` (key is ignored); thresholdv16 uses `key`. */
+int stg_codec_get_state(stg_codec_t h, const char *key, const void *key_ptr, float *threshold,
+                        float *threshold_inc, void *stream);
+
+/* Kernel timing, the GPU analogue of the reference's CRIT_PATH_compress stat
+ * span (engine/modules/compress.cpp:140-142, core_module_api.cpp:504-514):
+ * when enabled, every compress records HIP events on its stream around the
+ * codec's streaming pass ("scan") and its ordering/emission pass ("fill").
+ * stg_codec_get_timing synchronises the recorded events and returns the
+ * accumulated milliseconds [scan, fill, whole call] and the number of calls
+ * timed, then resets the accumulators. */
+int stg_codec_set_timing(stg_codec_t h, int enable);
+int stg_codec_get_timing(stg_codec_t h, double *ms3, uint64_t *calls);
+
+/* Checks the device-side failure word of every workspace of this handle
+ * (e.g. a regime-B candidate set larger than the build supports); syncs. */
+int stg_codec_check(stg_codec_t h);
+
+/* MERGE decompress (cpu_optimize.cpp:40-72): `world` rank streams of
+ * `per_rank` (idx, val) pairs each, laid out back to back, are scattered
+ * into a dense zeroed scratch of n floats in rank order (index_put_, no
+ * accumulate, per rank), summed, divided by `world`, and gathered at the
+ * union of indices.  Output is index-ascending; *d_out_count (device) gets
+ * the union size.  d_dense (n floats) and d_mark (n bytes) are caller
+ * scratch. */
+int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t per_rank, int world, size_t n,
+                             float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
+                             uint32_t *d_out_count, void *stream);
+
+/* Sparse SGD (optim/sgd.cpp:34-263 scalar path; options sgd.cpp:265-300).
+ * optimize_raw() keeps one momentum buffer per `name` on the device. */
+int stg_sgd_create(int device, float lr, float momentum, float dampening, float weight_decay, int nesterov,
+                   int maximize, stg_sgd_t *out);
+int stg_sgd_destroy(stg_sgd_t o);
+int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len,
+                                const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
+                                const uint32_t *d_grad_len, void *stream);
+int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_t len, void *stream);
+
+/* Synthetic fp32 buckets from the integer-only generator of SURVEY 8(d)
+ * (dist 0 = D1, 1 = D2 heavy tail, 2 = D3 zeros with prob param/1e4);
+ * bit-identical to oracle/stg_oracle.cpp:orc_synth_fill. */
+int stg_synth_fill_device(float *d_dst, size_t n, uint64_t seed, int dist, uint32_t param, void *stream);
+
+/* Thread-local message for the last failing call on this thread. */
+const char *stg_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STG_CODEC_H */

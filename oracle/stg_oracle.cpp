@@ -1,0 +1,444 @@
+/*
+ * stg_oracle.cpp -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Clean-room CPU restatement of StellaTrain's gradient-sparsification codec
+ * (reference snapshot 2024-08-07, backend/src/compress) plus the caller-side
+ * arithmetic (engine/modules/compress.cpp MERGE path), the MERGE decompress
+ * (engine/modules/cpu_optimize.cpp) and the scalar sparse-SGD loop
+ * (optim/sgd.cpp).  It is the *checker* for the HIP product path in
+ * stellatrain_amd/csrc and the "port" CPU baseline in bench.py.  Nothing in
+ * the product path may link or call this file.
+ *
+ * Parity pin: tests/test_oracle_golden.py checks this restatement bit-exactly
+ * against golden vectors produced by the reference sources themselves
+ * (oracle/_ref, built in place from /root/reference by oracle/Makefile;
+ * generator script tests/golden/make_golden.py).
+ *
+ * Semantics restated here (citations are /root/reference/backend/src/...):
+ *   - thresholdv16: compress/thresholdv16.cpp:22-29, 36-54, 57-73, 78-295
+ *   - threshold-v : compress/thresholdv.cpp:18-20, 27-37, 40-83, 292-293
+ *                   (the AVX-512 path is compiled out under -march=broadwell)
+ *   - top-k       : compress/topk.cpp:13-46 (incl. the byte-count memcpy bug)
+ *   - MERGE decompress: engine/modules/cpu_optimize.cpp:40-72
+ *   - sparse SGD  : optim/sgd.cpp:34-55, 221-263 (scalar path)
+ *
+ * The regime-B heap fill deliberately uses std::priority_queue: the
+ * reference's tie order among equal block sums *is* libstdc++'s
+ * make_heap/pop_heap order, so the oracle reproduces it by construction.
+ */
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <utility>
+#include <vector>
+
+#define ORC_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr uint32_t kLine = 16;  // floats per 64-byte cache line (thresholdv16.cpp:20)
+
+// ---------------------------------------------------------------------------
+// Synthetic inputs: integer-only generator, identical in
+// numpy (stellatrain_amd/synth.py) and on the device (csrc/synth.hip).
+// ---------------------------------------------------------------------------
+inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// thresholdv16
+// ---------------------------------------------------------------------------
+
+// |x| summed in the AVX tree order of hsum_float_avx (thresholdv16.cpp:57-73):
+// h(a) = ((a0+a4)+(a1+a5)) + ((a2+a6)+(a3+a7)); block = h(lo8) + h(hi8).
+inline float half_tree(const float *p) {
+    const float s04 = std::fabs(p[0]) + std::fabs(p[4]);
+    const float s15 = std::fabs(p[1]) + std::fabs(p[5]);
+    const float s26 = std::fabs(p[2]) + std::fabs(p[6]);
+    const float s37 = std::fabs(p[3]) + std::fabs(p[7]);
+    return (s04 + s15) + (s26 + s37);
+}
+inline float block_tree_sum(const float *p) { return half_tree(p) + half_tree(p + 8); }
+
+// thresholdv16.cpp:36-54: sequential per-block |x| sums, the last partial
+// block scaled by 16/(n%16), then the (k/16)-th largest (0-based).
+float tv16_first_threshold(const float *src, size_t n, uint32_t k) {
+    const size_t nblk = (n + kLine - 1) / kLine;
+    size_t bk = k / kLine;
+    std::vector<float> bs(nblk, 0.f);
+    for (size_t i = 0; i < n; ++i) bs[i / kLine] += std::fabs(src[i]);
+    if (n % kLine) bs[nblk - 1] *= static_cast<float>(kLine) / static_cast<float>(n % kLine);
+    if (bk >= nblk) bk = nblk - 1;  // reference reads past the end here (k == n); clamp
+    std::nth_element(bs.begin(), bs.begin() + bk, bs.end(),
+                     [](float a, float b) { return std::fabs(a) > std::fabs(b); });
+    return std::fabs(bs[bk]);
+}
+
+struct Tv16State {
+    float t;
+    float inc;
+};
+
+struct Tv16 {
+    std::mutex mu;
+    std::unordered_map<std::string, Tv16State> st;
+};
+
+// thresholdv16.cpp:78-295 restated (stage 1 / stage 2 / stage 3 / AIMD / heap).
+size_t tv16_compress(Tv16 *h, const std::string &name, const float *src, size_t n, uint32_t k,
+                     uint32_t *idx, size_t idx_cap, float *val, int32_t off) {
+    float t, inc;
+    bool have;
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        auto it = h->st.find(name);
+        have = it != h->st.end();
+        if (have) { t = it->second.t; inc = it->second.inc; }
+    }
+    if (!have) {
+        t = tv16_first_threshold(src, n, k);
+        inc = static_cast<float>(static_cast<double>(t) * 0.01);
+    }
+
+    const uint32_t dst_len = static_cast<uint32_t>(idx_cap);
+    const size_t nb = n / kLine;
+    const uint32_t tl = static_cast<uint32_t>(n % kLine);
+    const uint32_t d16 = dst_len - dst_len % kLine;
+    uint32_t cnt = 0;
+    size_t j = 0;
+    std::vector<std::pair<float, uint32_t>> cand;
+    cand.reserve(n / kLine + 1);
+
+    auto emit = [&](size_t pos, uint32_t len) {
+        for (uint32_t i = 0; i < len; ++i) {
+            idx[cnt + i] = static_cast<uint32_t>(pos + i) + static_cast<uint32_t>(off);
+            val[cnt + i] = src[pos + i];
+        }
+        cnt += len;
+    };
+
+    // stage 1: whole lines while at least one whole line of room remains
+    for (; j < nb && cnt < d16; ++j) {
+        const float s = block_tree_sum(src + j * kLine);
+        if (s >= t) emit(j * kLine, kLine);
+        else cand.emplace_back(s, static_cast<uint32_t>(j * kLine));
+    }
+    // stage 2: fewer than 16 slots left; first qualifying line donates a prefix
+    bool filled_in_stage2 = false;
+    if (j < nb && cnt < dst_len) {
+        const uint32_t rem = dst_len - cnt;
+        for (; j < nb; ++j) {
+            const float s = block_tree_sum(src + j * kLine);
+            if (s >= t) { emit(j * kLine, rem); filled_in_stage2 = true; break; }
+            cand.emplace_back(s, static_cast<uint32_t>(j * kLine));
+        }
+    }
+    // stage 3: ragged tail, judged on its *signed* sum (thresholdv16.cpp:212-236)
+    if (!filled_in_stage2 && tl != 0 && cnt < dst_len) {
+        const size_t p0 = nb * kLine;
+        const uint32_t rem = dst_len - cnt;
+        float s = 0.f;
+        for (uint32_t i = 0; i < tl; ++i) s += src[p0 + i];
+        if (s * static_cast<float>(kLine) >= t * static_cast<float>(tl)) {
+            emit(p0, std::min(rem, tl));
+        } else {
+            cand.emplace_back(s * static_cast<float>(kLine) / static_cast<float>(tl),
+                              static_cast<uint32_t>(p0));
+        }
+    }
+
+    // AIMD (thresholdv16.cpp:243-259)
+    if (cnt < dst_len) t = static_cast<float>(static_cast<double>(t) * 0.99);
+    else t = t + inc;
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        h->st[name] = Tv16State{t, inc};
+    }
+
+    // heap fill (thresholdv16.cpp:261-293): libstdc++ priority_queue order
+    if (cnt < dst_len) {
+        struct Less {
+            bool operator()(const std::pair<float, uint32_t> &a, const std::pair<float, uint32_t> &b) const {
+                return a.first < b.first;
+            }
+        };
+        std::priority_queue<std::pair<float, uint32_t>, std::vector<std::pair<float, uint32_t>>, Less> q(Less(), cand);
+        while (cnt < dst_len && !q.empty()) {
+            const uint32_t pos = q.top().second;
+            const uint32_t len = std::min(16u, std::min(static_cast<uint32_t>(n - pos), dst_len - cnt));
+            emit(pos, len);
+            q.pop();
+        }
+    }
+    return cnt;
+}
+
+// ---------------------------------------------------------------------------
+// threshold-v (naive path: thresholdv.cpp:40-83)
+// ---------------------------------------------------------------------------
+float tv_first_threshold(const float *src, size_t n, uint32_t k) {
+    std::vector<float> c(src, src + n);
+    size_t kk = std::min<size_t>(k, n - 1);  // reference reads c[n] when k == n; clamp
+    std::nth_element(c.begin(), c.begin() + kk, c.end(),
+                     [](float a, float b) { return std::fabs(a) > std::fabs(b); });
+    return std::fabs(c[kk]);
+}
+
+struct Tv {
+    std::mutex mu;
+    std::unordered_map<uint64_t, float> st;
+};
+
+size_t tv_compress(Tv *h, uint64_t key, const float *src, size_t n, uint32_t k, uint32_t *idx,
+                   size_t cap, float *val) {
+    float t;
+    bool have;
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        auto it = h->st.find(key);
+        have = it != h->st.end();
+        if (have) t = it->second;
+    }
+    if (!have) t = tv_first_threshold(src, n, k);
+
+    size_t cnt = 0;
+    float gmax = -1.f;
+    for (size_t i = 0; i < n; ++i) {
+        const float a = std::fabs(src[i]);
+        gmax = (a < gmax) ? gmax : a;  // std::max(a, gmax)
+        if (a >= t) {
+            if (cnt < cap) { idx[cnt] = static_cast<uint32_t>(i); val[cnt] = src[i]; }
+            ++cnt;
+        }
+    }
+    // AIMD; GCC -O3 -march=broadwell contracts the increase into one vfmadd231sd
+    if (k > cnt) t = static_cast<float>(static_cast<double>(t) * 0.99);
+    else if (k < cnt)
+        t = static_cast<float>(std::fma(0.01 * static_cast<double>(cnt) / static_cast<double>(k),
+                                         static_cast<double>(gmax), static_cast<double>(t)));
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        h->st[key] = t;
+    }
+    return std::min(cnt, cap);
+}
+
+// ---------------------------------------------------------------------------
+// Sparse SGD, scalar path (optim/sgd.cpp:34-55, 221-263), smart momentum off.
+// ---------------------------------------------------------------------------
+struct Sgd {
+    float lr = 1e-3f, momentum = 0.f, weight_decay = 0.f, dampening = 0.f;
+    bool nesterov = false, maximize = false;
+    uint32_t iter = 0;
+    std::mutex mu;
+    std::unordered_map<std::string, std::vector<float>> b;
+};
+
+void sgd_apply(Sgd *o, const std::string &name, float *param, uint32_t param_len, const float *g_in,
+               const uint32_t *gidx, uint32_t glen) {
+    bool first = false;
+    float *pb = nullptr;
+    {
+        std::lock_guard<std::mutex> g(o->mu);
+        if (o->momentum != 0.f && o->b.find(name) == o->b.end()) {
+            o->b[name].assign(param_len, 0.f);
+            first = true;
+        }
+        if (o->momentum != 0.f) pb = o->b[name].data();
+    }
+    const double lr = o->maximize ? -static_cast<double>(o->lr) : static_cast<double>(o->lr);
+    for (uint32_t i = 0; i < glen; ++i) {
+        const uint32_t id = gidx[i];
+        const float x = param[id];
+        float g = g_in[i];
+        const float m = o->momentum;
+        if (o->weight_decay != 0.f) g = std::fmaf(o->weight_decay, x, g);
+        if (o->momentum != 0.f) {
+            float bnew;
+            if (!first) bnew = std::fmaf(pb[id], m, (1.f - o->dampening) * g);
+            else bnew = g;
+            if (o->nesterov) g = std::fmaf(m, bnew, g);
+            else g = bnew;
+            pb[id] = bnew;
+        }
+        param[id] = static_cast<float>(std::fma(-lr, static_cast<double>(g), static_cast<double>(x)));
+    }
+    o->iter++;
+}
+
+thread_local std::string g_err;
+
+}  // namespace
+
+// ===========================================================================
+// C ABI of the oracle (consumed by tests/ and bench.py's cpu_baseline only)
+// ===========================================================================
+
+ORC_API void orc_synth_fill(float *dst, size_t n, uint64_t seed, int dist, uint32_t param) {
+    // dist 0: D1 Irwin-Hall(4) of 24-bit uniforms, centred, * 2^-24 * 1e-3
+    // dist 1: D2 = D1 * 2^-e, e = U{0..8}
+    // dist 2: D3 = D1 with zeros; param = zero probability in units of 1e-4
+    const double scale = 1e-3 / 16777216.0;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t base = seed * 0x100000001B3ull + static_cast<uint64_t>(i) * 4u;
+        const uint64_t r0 = splitmix64(base + 0), r1 = splitmix64(base + 1);
+        const int64_t v = static_cast<int64_t>(r0 & 0xFFFFFF) + static_cast<int64_t>((r0 >> 24) & 0xFFFFFF) +
+                          static_cast<int64_t>(r1 & 0xFFFFFF) + static_cast<int64_t>((r1 >> 24) & 0xFFFFFF) -
+                          (int64_t{1} << 25);
+        double x = static_cast<double>(v) * scale;
+        if (dist == 1) {
+            const uint32_t e = static_cast<uint32_t>((r1 >> 48) % 9u);
+            x = std::ldexp(x, -static_cast<int>(e));
+        } else if (dist == 2) {
+            const uint32_t z = static_cast<uint32_t>((r0 >> 48) % 10000u);
+            if (z < param) x = 0.0;
+        }
+        dst[i] = static_cast<float>(x);
+    }
+}
+
+ORC_API const char *orc_last_error(void) { return g_err.c_str(); }
+
+// --- thresholdv16 ---
+ORC_API void *orc_tv16_new(void) { return new Tv16(); }
+ORC_API void orc_tv16_free(void *h) { delete static_cast<Tv16 *>(h); }
+ORC_API size_t orc_tv16_compress(void *h, const char *name, const float *src, size_t n, uint32_t k,
+                                 uint32_t *idx, size_t idx_cap, float *val, int32_t idx_offset) {
+    return tv16_compress(static_cast<Tv16 *>(h), name, src, n, k, idx, idx_cap, val, idx_offset);
+}
+ORC_API int orc_tv16_state(void *h, const char *name, float *t, float *inc) {
+    auto *p = static_cast<Tv16 *>(h);
+    std::lock_guard<std::mutex> g(p->mu);
+    auto it = p->st.find(name);
+    if (it == p->st.end()) return -1;
+    *t = it->second.t;
+    *inc = it->second.inc;
+    return 0;
+}
+ORC_API float orc_tv16_first_threshold(const float *src, size_t n, uint32_t k) {
+    return tv16_first_threshold(src, n, k);
+}
+ORC_API void orc_tv16_block_sums(const float *src, size_t n, float *out) {
+    for (size_t j = 0; j < n / kLine; ++j) out[j] = block_tree_sum(src + j * kLine);
+}
+
+// --- threshold-v (state keyed by the caller's src pointer in the reference;
+//     here the key is explicit so tests can emulate the engine's two buffers) ---
+ORC_API void *orc_tv_new(void) { return new Tv(); }
+ORC_API void orc_tv_free(void *h) { delete static_cast<Tv *>(h); }
+ORC_API size_t orc_tv_compress(void *h, uint64_t key, const float *src, size_t n, uint32_t k,
+                               uint32_t *idx, size_t cap, float *val) {
+    return tv_compress(static_cast<Tv *>(h), key, src, n, k, idx, cap, val);
+}
+ORC_API int orc_tv_state(void *h, uint64_t key, float *t) {
+    auto *p = static_cast<Tv *>(h);
+    std::lock_guard<std::mutex> g(p->mu);
+    auto it = p->st.find(key);
+    if (it == p->st.end()) return -1;
+    *t = it->second;
+    return 0;
+}
+ORC_API float orc_tv_first_threshold(const float *src, size_t n, uint32_t k) {
+    return tv_first_threshold(src, n, k);
+}
+
+// --- top-k (topk.cpp:28-46).  bug_compat=1 reproduces the byte-count memcpy
+//     (only n bytes = n/4 floats survive) and idx = 0..k-1, in libstdc++
+//     nth_element partition order; bug_compat=0 is the intended top-k by |x|
+//     over the whole bucket with real indices (+idx_offset), index-ordered. ---
+ORC_API int64_t orc_topk_compress(const float *src, size_t n, uint32_t k, uint32_t *idx, size_t cap,
+                                  float *val, int32_t idx_offset, int bug_compat) {
+    if (cap < k) { g_err = "Invalid parameter k"; return -1; }
+    if (bug_compat) {
+        std::vector<float> c(n, 0.f);
+        std::memcpy(c.data(), src, n);  // sic: bytes, not floats (topk.cpp:31)
+        std::nth_element(c.begin(), c.begin() + std::min<size_t>(k, n), c.end(),
+                         [](float a, float b) { return std::fabs(a) > std::fabs(b); });
+        for (uint32_t i = 0; i < k; ++i) { idx[i] = i; val[i] = c[i]; }
+        return static_cast<int64_t>(cap);
+    }
+    std::vector<uint32_t> order(n);
+    for (size_t i = 0; i < n; ++i) order[i] = static_cast<uint32_t>(i);
+    // rank by |x| desc, ties by index asc; emit the k winners in index order
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return std::fabs(src[a]) > std::fabs(src[b]); });
+    std::vector<uint32_t> win(order.begin(), order.begin() + std::min<size_t>(k, n));
+    std::sort(win.begin(), win.end());
+    for (size_t i = 0; i < win.size(); ++i) {
+        idx[i] = win[i] + static_cast<uint32_t>(idx_offset);
+        val[i] = src[win[i]];
+    }
+    return static_cast<int64_t>(cap);
+}
+
+// --- MERGE caller arithmetic (compress.cpp:44,52) and API k (core.cpp:1216) ---
+ORC_API int64_t orc_merge_numel(int64_t n, double ratio, int world) {
+    // compression_ratio_ is double (core.h:96), world is cast to float, the
+    // quotient is stored in a float, and size_t * float is a float product.
+    const float kf = static_cast<float>((1 - ratio) / static_cast<float>(world));
+    const int64_t lo = std::min<int64_t>(n, 1);
+    return std::max<int64_t>(lo, static_cast<int64_t>(static_cast<float>(n) * kf));
+}
+ORC_API int64_t orc_api_numel(int64_t n, float ratio) {
+    return static_cast<int64_t>((1. - static_cast<double>(ratio)) * static_cast<double>(n));
+}
+
+// --- MERGE decompress (cpu_optimize.cpp:40-72): per-rank dense scatter
+//     (index_put_, no accumulate), rank-order sum, /world, unique union of
+//     indices, gather.  Output is sorted by index (the reference's
+//     unordered_set order is unspecified; SGD is per-index so order is moot). ---
+ORC_API size_t orc_merge_decompress(const uint32_t *idx, const float *val, size_t per_rank, int world,
+                                    size_t n, uint32_t *out_idx, float *out_val) {
+    std::vector<float> merged(n, 0.f);
+    std::vector<float> tmp(n);
+    std::vector<char> seen(n, 0);
+    for (int r = 0; r < world; ++r) {
+        std::fill(tmp.begin(), tmp.end(), 0.f);
+        for (size_t i = 0; i < per_rank; ++i) tmp[idx[r * per_rank + i]] = val[r * per_rank + i];
+        for (size_t i = 0; i < n; ++i) merged[i] += tmp[i];
+        for (size_t i = 0; i < per_rank; ++i) seen[idx[r * per_rank + i]] = 1;
+    }
+    const float w = static_cast<float>(world);
+    size_t m = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (!seen[i]) continue;
+        out_idx[m] = static_cast<uint32_t>(i);
+        out_val[m] = merged[i] / w;
+        ++m;
+    }
+    return m;
+}
+
+// --- sparse SGD ---
+ORC_API void *orc_sgd_new(float lr, float momentum, float dampening, float weight_decay, int nesterov,
+                          int maximize) {
+    auto *o = new Sgd();
+    o->lr = lr; o->momentum = momentum; o->dampening = dampening; o->weight_decay = weight_decay;
+    o->nesterov = nesterov != 0; o->maximize = maximize != 0;
+    return o;
+}
+ORC_API void orc_sgd_free(void *o) { delete static_cast<Sgd *>(o); }
+ORC_API void orc_sgd_apply(void *o, const char *name, float *param, uint32_t param_len, const float *g,
+                           const uint32_t *gidx, uint32_t glen) {
+    sgd_apply(static_cast<Sgd *>(o), name, param, param_len, g, gidx, glen);
+}
+ORC_API int orc_sgd_momentum(void *o, const char *name, float *out, uint32_t len) {
+    auto *p = static_cast<Sgd *>(o);
+    std::lock_guard<std::mutex> g(p->mu);
+    auto it = p->b.find(name);
+    if (it == p->b.end()) return -1;
+    std::memcpy(out, it->second.data(), sizeof(float) * std::min<size_t>(len, it->second.size()));
+    return 0;
+}

@@ -1,0 +1,177 @@
+"""Host-side mirror of the reference codec interface, over the HIP C-ABI.
+
+Reference interface (``/root/reference/backend/src/compress/compressor.h:12-31``)::
+
+    class Compressor {
+        Compressor(std::unique_ptr<ThreadPool> &thread_pool, std::string name);
+        const std::string &name();
+        virtual size_t compress(const std::string &name, ConstSegment<float> src, uint32_t k,
+                                Segment<uint32_t> dst_idx, Segment<float> dst_val,
+                                int32_t idx_offset = 0) = 0;
+    };
+
+``ConstSegment``/``Segment`` (pointer, length) pairs become 1-D tensors or
+arrays whose length is the segment length.  Device tensors run the
+device-resident path on torch's current HIP stream; host tensors/arrays run
+the host path (copy in, compress on the GPU, copy out).  ``compress`` returns
+the reference's ``size_t`` (so it synchronises for device inputs);
+``compress_async`` returns the count as a device tensor and never syncs.
+Errors raise ``RuntimeError`` (``CodecError``), as the reference throws
+``std::runtime_error`` (topk.cpp:34, core.cpp:117,193).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._capi import CodecError, check, lib
+
+__all__ = ["Compressor", "ThresholdvCompressor16", "ThresholdvCompressor", "TopkCompressor", "make_compressor",
+           "CodecError"]
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _stream_ptr(device: int) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Compressor:
+    """Base class: one C-ABI codec handle (``stg_codec_create``)."""
+
+    _method = ""
+
+    def __init__(self, thread_pool=None, *, device: int = 0, method: str | None = None):
+        # thread_pool: accepted for signature parity (compressor.h:26); the GPU
+        # codec needs no host pool.
+        self.thread_pool_ = thread_pool
+        self.device = device
+        self._method = method or self._method
+        h = C.c_void_p()
+        check(lib().stg_codec_create(self._method.encode(), device, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().stg_codec_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def name(self) -> str:
+        """``Compressor::name()`` (compressor.h:28)."""
+        return lib().stg_codec_name(self._h).decode()
+
+    # -- compress ----------------------------------------------------------
+    def compress(self, name: str, src, k: int, dst_idx, dst_val, idx_offset: int = 0) -> int:
+        """``Compressor::compress`` (compressor.h:30); returns the pair count."""
+        if _is_torch(src) and src.is_cuda:
+            cnt = self.compress_async(name, src, k, dst_idx, dst_val, idx_offset)
+            return int(cnt.item())
+        return self._compress_host(name, src, k, dst_idx, dst_val, idx_offset)
+
+    def compress_async(self, name: str, src, k: int, dst_idx, dst_val, idx_offset: int = 0, count=None):
+        """Device-resident compress on torch's current stream; returns a 1-element
+        uint32-valued int32 tensor holding the count (no host sync)."""
+        import torch
+        assert src.is_cuda and dst_idx.is_cuda and dst_val.is_cuda, "device path needs device tensors"
+        assert src.dtype == torch.float32 and dst_val.dtype == torch.float32
+        assert dst_idx.dtype in (torch.int32, torch.uint32)
+        assert src.is_contiguous() and dst_idx.is_contiguous() and dst_val.is_contiguous()
+        if count is None:
+            count = torch.empty(1, dtype=torch.int32, device=src.device)
+        check(lib().stg_codec_compress_device(
+            self._h, name.encode(), C.c_void_p(src.data_ptr()), src.numel(), int(k),
+            C.c_void_p(dst_idx.data_ptr()), dst_idx.numel(), C.c_void_p(dst_val.data_ptr()), dst_val.numel(),
+            int(idx_offset), C.c_void_p(count.data_ptr()), C.c_void_p(_stream_ptr(src.device.index))))
+        return count
+
+    def _compress_host(self, name, src, k, dst_idx, dst_val, idx_offset) -> int:
+        s = src.numpy() if _is_torch(src) else src
+        di = dst_idx.numpy() if _is_torch(dst_idx) else dst_idx
+        dv = dst_val.numpy() if _is_torch(dst_val) else dst_val
+        if not (isinstance(s, np.ndarray) and s.dtype == np.float32 and s.flags.c_contiguous):
+            raise TypeError("src must be a contiguous float32 array/tensor")
+        if di.dtype.itemsize != 4 or dv.dtype != np.float32 or not di.flags.c_contiguous or not dv.flags.c_contiguous:
+            raise TypeError("dst_idx must be contiguous (u)int32 and dst_val contiguous float32")
+        out = C.c_size_t()
+        check(lib().stg_codec_compress_host(
+            self._h, name.encode(), C.c_void_p(s.ctypes.data), s.size, int(k), C.c_void_p(di.ctypes.data),
+            di.size, C.c_void_p(dv.ctypes.data), dv.size, int(idx_offset), C.byref(out)))
+        return int(out.value)
+
+    # -- introspection (tests) ----------------------------------------------
+    def state(self, name: str = "", key_ptr: int = 0, stream=None):
+        """Per-key AIMD state (threshold, threshold_inc) or None if never seen."""
+        t, inc = C.c_float(), C.c_float()
+        sp = stream if stream is not None else 0
+        rc = lib().stg_codec_get_state(self._h, name.encode(), C.c_void_p(key_ptr), C.byref(t), C.byref(inc),
+                                       C.c_void_p(sp))
+        if rc != 0:
+            return None
+        return t.value, inc.value
+
+    def set_timing(self, enable: bool) -> None:
+        check(lib().stg_codec_set_timing(self._h, int(enable)))
+
+    def get_timing(self):
+        """(scan_ms, fill_ms, call_ms) accumulated since the last read, and calls."""
+        ms = (C.c_double * 3)()
+        calls = C.c_uint64()
+        check(lib().stg_codec_get_timing(self._h, ms, C.byref(calls)))
+        return (ms[0], ms[1], ms[2]), int(calls.value)
+
+    def check_device(self) -> None:
+        check(lib().stg_codec_check(self._h))
+
+
+class ThresholdvCompressor16(Compressor):
+    """``ThresholdvCompressor16(std::unique_ptr<ThreadPool>&, bool multicore=true)``
+    (thresholdv16.h:33-34); per-name AIMD state (thresholdv16.cpp:81-97)."""
+
+    _method = "thresholdv16"
+
+    def __init__(self, thread_pool=None, multicore: bool = True, *, device: int = 0):
+        self.multicore_ = multicore  # never read by the reference either
+        super().__init__(thread_pool, device=device)
+
+
+class ThresholdvCompressor(Compressor):
+    """``ThresholdvCompressor(std::unique_ptr<ThreadPool>&, bool multicore=true)``
+    (thresholdv.h:24-25); AIMD state keyed by the src pointer (thresholdv.cpp:44)."""
+
+    _method = "thresholdv"
+
+    def __init__(self, thread_pool=None, multicore: bool = True, *, device: int = 0):
+        self.multicore_ = multicore
+        super().__init__(thread_pool, device=device)
+
+
+class TopkCompressor(Compressor):
+    """``TopkCompressor(std::unique_ptr<ThreadPool>&)`` (topk.h:28-29).  ``exact=False``
+    keeps the shipped behaviour (byte-count memcpy, idx 0..k-1: topk.cpp:31,42);
+    ``exact=True`` is the intended top-k by |x| with real indices."""
+
+    _method = "topk"
+
+    def __init__(self, thread_pool=None, *, exact: bool = False, device: int = 0):
+        super().__init__(thread_pool, device=device, method="topk_exact" if exact else "topk")
+
+
+def make_compressor(method: str, thread_pool=None, *, device: int = 0) -> Compressor:
+    """Factory of FasterDpEngine::configure (core.cpp:110-118)."""
+    if method == "thresholdv":
+        return ThresholdvCompressor(thread_pool, True, device=device)
+    if method == "thresholdv16":
+        return ThresholdvCompressor16(thread_pool, True, device=device)
+    if method == "topk":
+        return TopkCompressor(thread_pool, device=device)
+    if method == "topk_exact":
+        return TopkCompressor(thread_pool, exact=True, device=device)
+    raise CodecError(-2, f"Unknown compression method {method}.")

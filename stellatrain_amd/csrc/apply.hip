@@ -1,0 +1,168 @@
+// apply.hip -- inverse path of config 5: MERGE decompress + sparse SGD (gfx950).
+//
+// MERGE decompress: engine/modules/cpu_optimize.cpp:40-72.  For each of
+// `world` rank streams: tmp = zeros(n); tmp.index_put_(idx_r, val_r);
+// merged += tmp (rank order); merged /= float(world); the output is merged
+// gathered at the union of the indices.  Within a rank the codec's indices
+// are unique, so a plain (non-atomic) add per rank, launched in rank order,
+// reproduces the rank-ordered float sum exactly (adding the +0.0 of ranks that
+// miss an index never changes a finite sum; the first add maps -0.0 to +0.0
+// exactly as 0 + v does).  The output is index-ascending (the reference's
+// unordered_set order is unspecified and SGD is per-index).  world == 1 needs
+// no dense scratch: out = (0.0f + v) / 1.0f in stream order.
+//
+// Sparse SGD: optim/sgd.cpp:34-55 and the scalar loop :221-263 with the FMA
+// shapes GCC -O3 -march=broadwell emits (read from the object code):
+//   wd:        g = fmaf(wd, x, g)                        (vfmadd231ss, :235)
+//   momentum:  b = first ? g : fmaf(b_old, m, (1-d)*g)   (vfmadd231ss, :242)
+//   nesterov:  g = fmaf(m, b, g)  else g = b             (vfmadd231ss, :247)
+//   update:    x = (float)fma(-lr, (double)g, (double)x) (vfnmadd231sd, :256)
+#include <algorithm>
+
+#include "ws.h"
+
+namespace stg {
+
+namespace {
+
+constexpr uint32_t MARK_TILE = STG_WG * 16;  // marks per tile (one uint4 per lane)
+
+__global__ void __launch_bounds__(STG_WG) merge_world1(const uint32_t *__restrict__ idx, const float *__restrict__ val,
+                                                       size_t m, uint32_t *__restrict__ out_idx,
+                                                       float *__restrict__ out_val, uint32_t *out_count) {
+    const size_t stride = (size_t)gridDim.x * STG_WG;
+    for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
+        out_idx[i] = idx[i];
+        out_val[i] = (0.0f + val[i]) / 1.0f;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = (uint32_t)m;
+}
+
+__global__ void __launch_bounds__(STG_WG) scatter_rank(const uint32_t *__restrict__ idx, const float *__restrict__ val,
+                                                       size_t m, float *__restrict__ dense, uint8_t *__restrict__ mark) {
+    const size_t stride = (size_t)gridDim.x * STG_WG;
+    for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
+        const uint32_t j = idx[i];
+        dense[j] += val[i];
+        mark[j] = 1;
+    }
+}
+
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t w) {
+    uint32_t c = 0;
+    c += (w & 0xffu) != 0;
+    c += (w & 0xff00u) != 0;
+    c += (w & 0xff0000u) != 0;
+    c += (w & 0xff000000u) != 0;
+    return c;
+}
+
+__device__ __forceinline__ uint4 load_marks(const uint8_t *mark, size_t n, size_t e) {
+    if (e + 16 <= n) return *reinterpret_cast<const uint4 *>(mark + e);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t b = 0; b < 16; ++b)
+        if (e + b < n) w[b >> 2] |= (uint32_t)mark[e + b] << (8 * (b & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ void __launch_bounds__(STG_WG) mark_count(const uint8_t *__restrict__ mark, size_t n,
+                                                     uint32_t *__restrict__ tile_cnt) {
+    __shared__ uint32_t s[STG_WAVES];
+    const size_t e = (size_t)blockIdx.x * MARK_TILE + 16 * threadIdx.x;
+    const uint4 v = load_marks(mark, n, e);
+    uint32_t c = nz_bytes(v.x) + nz_bytes(v.y) + nz_bytes(v.z) + nz_bytes(v.w);
+    c = wave_sum(c);
+    if (__lane_id() == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) t += s[w];
+        tile_cnt[blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(STG_WG) mark_emit(uint8_t *__restrict__ mark, float *__restrict__ dense, size_t n,
+                                                    uint32_t ntiles, float world, const uint32_t *__restrict__ tile_cnt,
+                                                    uint32_t *__restrict__ out_idx, float *__restrict__ out_val,
+                                                    uint32_t *out_count) {
+    __shared__ uint64_t sh64[STG_WAVES];
+    __shared__ uint32_t sh[STG_WAVES + 1];
+    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+    const uint32_t t_begin = (uint32_t)((uint64_t)w * ntiles / G);
+    const uint32_t t_end = (uint32_t)((uint64_t)(w + 1) * ntiles / G);
+    uint64_t tot = 0, bef = 0;
+    for (uint32_t i = tid; i < ntiles; i += STG_WG) {
+        const uint32_t c = tile_cnt[i];
+        tot += c;
+        if (i < t_begin) bef += c;
+    }
+    const uint64_t total = wg_sum64(tot, sh64);
+    uint64_t P = wg_sum64(bef, sh64);
+    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+        const size_t e = (size_t)tile * MARK_TILE + 16 * tid;
+        const uint4 v = load_marks(mark, n, e);
+        const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+        uint32_t c = nz_bytes(v.x) + nz_bytes(v.y) + nz_bytes(v.z) + nz_bytes(v.w);
+        uint32_t tc;
+        uint32_t r = wg_excl_scan(c, sh, &tc);
+        for (uint32_t b = 0; b < 16; ++b) {
+            if ((words[b >> 2] >> (8 * (b & 3))) & 0xffu) {
+                const size_t j = e + b;
+                out_idx[P + r] = (uint32_t)j;
+                out_val[P + r] = dense[j] / world;
+                dense[j] = 0.f;  // leave the scratch zeroed for the next call
+                mark[j] = 0;
+                ++r;
+            }
+        }
+        P += tc;
+    }
+    if (w == 0 && tid == 0) *out_count = (uint32_t)total;
+}
+
+__global__ void __launch_bounds__(STG_WG) sgd_apply(SgdLaunch a) {
+    uint32_t len = a.grad_len;
+    if (a.d_grad_len) len = min(len, *a.d_grad_len);
+    const uint32_t stride = gridDim.x * STG_WG;
+    for (uint32_t i = blockIdx.x * STG_WG + threadIdx.x; i < len; i += stride) {
+        const uint32_t id = a.gidx[i];
+        const float x = a.param[id];
+        float g = a.grad[i];
+        if (a.weight_decay != 0.f) g = fmaf(a.weight_decay, x, g);
+        if (a.mom) {
+            const float b = a.first ? g : fmaf(a.mom[id], a.momentum, (1.0f - a.dampening) * g);
+            g = a.nesterov ? fmaf(a.momentum, b, g) : b;
+            a.mom[id] = b;
+        }
+        a.param[id] = (float)fma(-a.lr, (double)g, (double)x);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
+                                float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,
+                                uint32_t *out_count, uint32_t *scratch_tiles, int num_cu, hipStream_t s) {
+    const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((per_rank + STG_WG - 1) / STG_WG,
+                                                                          (size_t)num_cu * 8));
+    if (world == 1) {
+        merge_world1<<<blocks, STG_WG, 0, s>>>(idx, val, per_rank, out_idx, out_val, out_count);
+        return hipGetLastError();
+    }
+    for (int r = 0; r < world; ++r)
+        scatter_rank<<<blocks, STG_WG, 0, s>>>(idx + (size_t)r * per_rank, val + (size_t)r * per_rank, per_rank,
+                                               dense, mark);
+    const uint32_t ntiles = (uint32_t)((n + MARK_TILE - 1) / MARK_TILE);
+    mark_count<<<std::max<uint32_t>(1, ntiles), STG_WG, 0, s>>>(mark, n, scratch_tiles);
+    const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)num_cu, ntiles));
+    mark_emit<<<G, STG_WG, 0, s>>>(mark, dense, n, ntiles, (float)world, scratch_tiles, out_idx, out_val, out_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_sgd(const SgdLaunch &a, hipStream_t s) {
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((a.grad_len + STG_WG - 1) / STG_WG, 2048));
+    sgd_apply<<<blocks, STG_WG, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+}  // namespace stg

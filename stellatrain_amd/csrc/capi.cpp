@@ -1,0 +1,542 @@
+// capi.cpp -- host side of the C-ABI declared in include/stg/codec.h.
+//
+// Owns: codec handles (method, device), the per-key AIMD state slots (device
+// resident, 16 B each, in never-moving chunks), and one workspace per HIP
+// stream.  The reference keeps the threshold maps in the compressor object
+// behind a mutex (thresholdv16.h:11-14, thresholdv16.cpp:84-91,255-258) and
+// is called concurrently from up to 32 ThreadPool workers on different keys
+// (engine/config.h:7, core_module_api.cpp:7-24); here every call locks the
+// handle only to look up its slot and its stream's workspace, and the launch
+// sequence of one call holds that workspace's lock so calls sharing a stream
+// cannot interleave their kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/stg/codec.h"
+#include "ws.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(STG_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+enum Method { M_TV16 = 0, M_TV = 1, M_TOPK = 2, M_TOPK_EXACT = 3 };
+
+constexpr uint32_t SLOTS_PER_CHUNK = 4096;
+
+struct Workspace {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    stg::DevWS d{};
+    void *fixed = nullptr;
+    size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0;
+    // device buffers of the host-memory entry point
+    float *h_src = nullptr;
+    size_t cap_src = 0;
+    uint32_t *h_idx = nullptr;
+    float *h_val = nullptr;
+    size_t cap_out = 0;
+    uint32_t *h_count = nullptr;
+    uint32_t *pinned_count = nullptr;
+
+    ~Workspace() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        (void)hipFree(fixed);
+        (void)hipFree(d.sums);
+        (void)hipFree(d.tile_cnt);
+        (void)hipFree(d.tile_aux);
+        (void)hipFree(d.stage_pos);
+        (void)hipFree(d.stage_val);
+        (void)hipFree(h_src);
+        (void)hipFree(h_idx);
+        (void)hipFree(h_val);
+        (void)hipFree(h_count);
+        if (pinned_count) (void)hipHostFree(pinned_count);
+    }
+
+    int init() {
+        size_t off = 0;
+        auto carve = [&](size_t bytes) {
+            const size_t o = off;
+            off = (off + bytes + 255) & ~size_t(255);
+            return o;
+        };
+        const size_t o_ctl = carve(sizeof(stg::FillCtl));
+        const size_t o_cp = carve(sizeof(stg::CallParams));
+        const size_t o_rs = carve(sizeof(stg::RSel));
+        const size_t o_fail = carve(sizeof(uint32_t));
+        const size_t o_cand = carve(sizeof(uint64_t) * stg::SORT_CAP);
+        const size_t o_misc = carve(sizeof(uint32_t) * 64);
+        HIP_TRY(hipMalloc(&fixed, off));
+        HIP_TRY(hipMemset(fixed, 0, off));
+        char *b = static_cast<char *>(fixed);
+        d.ctl = reinterpret_cast<stg::FillCtl *>(b + o_ctl);
+        d.cp = reinterpret_cast<stg::CallParams *>(b + o_cp);
+        d.rsel = reinterpret_cast<stg::RSel *>(b + o_rs);
+        d.fail = reinterpret_cast<uint32_t *>(b + o_fail);
+        d.cand = reinterpret_cast<uint64_t *>(b + o_cand);
+        d.misc = reinterpret_cast<uint32_t *>(b + o_misc);
+        return STG_OK;
+    }
+
+    // Grow-only scratch.  Growing waits for this stream's in-flight work.
+    template <typename T>
+    int grow(T *&p, size_t &cap, size_t need) {
+        if (need <= cap) return STG_OK;
+        HIP_TRY(hipStreamSynchronize(stream));
+        (void)hipFree(p);
+        p = nullptr;
+        const size_t n = std::max<size_t>(need, cap + cap / 2);
+        HIP_TRY(hipMalloc(&p, n * sizeof(T)));
+        cap = n;
+        return STG_OK;
+    }
+
+    int ensure(size_t sums, size_t tiles, size_t stage) {
+        int rc;
+        if ((rc = grow(d.sums, cap_sums, sums))) return rc;
+        size_t ct = cap_tiles;
+        if ((rc = grow(d.tile_cnt, ct, tiles))) return rc;
+        ct = cap_tiles;
+        if ((rc = grow(d.tile_aux, ct, tiles))) return rc;
+        cap_tiles = ct;
+        size_t cs = cap_stage;
+        if ((rc = grow(d.stage_pos, cs, stage))) return rc;
+        cs = cap_stage;
+        if ((rc = grow(d.stage_val, cs, stage))) return rc;
+        cap_stage = cs;
+        return STG_OK;
+    }
+};
+
+}  // namespace
+
+struct stg_codec {
+    Method method;
+    int device = 0;
+    int num_cu = 256;
+    std::string name;
+    std::mutex mu;
+    std::unordered_map<std::string, uint32_t> slot_of;
+    std::vector<KeyState *> chunks;
+    uint32_t nslots = 0;
+    std::unordered_map<hipStream_t, std::unique_ptr<Workspace>> ws;
+    // kernel timing (stg_codec_set_timing)
+    bool timing = false;
+    std::vector<std::array<hipEvent_t, 3>> ev_pending, ev_pool;
+    double ms_acc[3] = {0, 0, 0};
+    uint64_t timed_calls = 0;
+
+    ~stg_codec() {
+        (void)hipSetDevice(device);
+        ws.clear();
+        for (auto *c : chunks) (void)hipFree(c);
+        for (auto *v : {&ev_pending, &ev_pool})
+            for (auto &e : *v)
+                for (auto x : e) (void)hipEventDestroy(x);
+    }
+
+    // Events for one timed call (nullptr when timing is off).
+    int take_events(std::array<hipEvent_t, 3> *e, bool *on) {
+        std::lock_guard<std::mutex> g(mu);
+        *on = timing;
+        if (!timing) return STG_OK;
+        if (!ev_pool.empty()) { *e = ev_pool.back(); ev_pool.pop_back(); }
+        else for (auto &x : *e) HIP_TRY(hipEventCreate(&x));
+        ev_pending.push_back(*e);
+        return STG_OK;
+    }
+
+    KeyState *slot_ptr(uint32_t s) { return chunks[s / SLOTS_PER_CHUNK] + (s % SLOTS_PER_CHUNK); }
+
+    // Returns the state slot of `key`; *fresh = true when it was just created.
+    int slot(const std::string &key, KeyState **out, bool *fresh) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = slot_of.find(key);
+        if (it != slot_of.end()) { *out = slot_ptr(it->second); *fresh = false; return STG_OK; }
+        if (nslots % SLOTS_PER_CHUNK == 0) {
+            KeyState *c = nullptr;
+            HIP_TRY(hipMalloc(&c, sizeof(KeyState) * SLOTS_PER_CHUNK));
+            HIP_TRY(hipMemset(c, 0, sizeof(KeyState) * SLOTS_PER_CHUNK));
+            chunks.push_back(c);
+        }
+        const uint32_t s = nslots++;
+        slot_of.emplace(key, s);
+        *out = slot_ptr(s);
+        *fresh = true;
+        return STG_OK;
+    }
+
+    int workspace(hipStream_t s, Workspace **out) {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = ws.find(s);
+        if (it != ws.end()) { *out = it->second.get(); return STG_OK; }
+        auto w = std::make_unique<Workspace>();
+        w->device = device;
+        w->stream = s;
+        int rc = w->init();
+        if (rc) return rc;
+        *out = w.get();
+        ws.emplace(s, std::move(w));
+        return STG_OK;
+    }
+};
+
+struct stg_sgd {
+    int device = 0;
+    float lr, momentum, dampening, weight_decay;
+    bool nesterov, maximize;
+    uint32_t iter = 0;
+    std::mutex mu;
+    std::unordered_map<std::string, std::pair<float *, uint32_t>> mom;
+    ~stg_sgd() {
+        (void)hipSetDevice(device);
+        for (auto &kv : mom) (void)hipFree(kv.second.first);
+    }
+};
+
+namespace {
+
+std::string state_key(Method m, const char *key, const void *src) {
+    if (m == M_TV) {  // thresholdv.cpp:44: keyed by the src pointer
+        char b[32];
+        snprintf(b, sizeof b, "\x01%p", src);
+        return b;
+    }
+    return key ? std::string(key) : std::string();
+}
+
+thread_local std::unordered_map<int, hipStream_t> t_streams;
+
+int thread_stream(int device, hipStream_t *s) {
+    auto it = t_streams.find(device);
+    if (it != t_streams.end()) { *s = it->second; return STG_OK; }
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    t_streams.emplace(device, st);
+    *s = st;
+    return STG_OK;
+}
+
+int run_device(stg_codec *h, const char *key, const float *d_src, const void *key_ptr, size_t n, uint32_t k,
+               uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset, uint32_t *d_count,
+               hipStream_t s) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    if (val_cap < idx_cap) return fail(STG_ERR_INVALID, "value capacity smaller than index capacity");
+    if ((h->method == M_TOPK || h->method == M_TOPK_EXACT) && idx_cap < k)
+        return fail(STG_ERR_INVALID, "Invalid parameter k");  // topk.cpp:33-34
+    if (n >= (size_t(1) << 32) || idx_cap >= (size_t(1) << 32))
+        return fail(STG_ERR_UNSUPPORTED, "bucket larger than 2^32-1 elements (uint32 indices)");
+    if (!d_count) return fail(STG_ERR_INVALID, "null count pointer");
+    HIP_TRY(hipSetDevice(h->device));
+    Workspace *ws = nullptr;
+    int rc = h->workspace(s, &ws);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(ws->mu);
+    if (n == 0) {
+        HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(uint32_t), s));
+        return STG_OK;
+    }
+    std::array<hipEvent_t, 3> evs{};
+    bool timed = false;
+    if ((rc = h->take_events(&evs, &timed))) return rc;
+    hipEvent_t *ev = timed ? evs.data() : nullptr;
+    if (h->method == M_TV16) {
+        KeyState *st;
+        bool fresh;
+        if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
+        const size_t nblk = (n + 15) / 16;
+        const size_t ntiles = (n / 16 + stg::TV16_TILE_BLOCKS - 1) / stg::TV16_TILE_BLOCKS;
+        if ((rc = ws->ensure(nblk, std::max<size_t>(ntiles, 1), 1))) return rc;
+        stg::Tv16Launch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, d_count, st, fresh, h->num_cu, ev};
+        HIP_TRY(stg::launch_tv16(a, ws->d, s));
+    } else if (h->method == M_TV) {
+        KeyState *st;
+        bool fresh;
+        if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
+        const size_t ntiles = (n + stg::TV_TILE - 1) / stg::TV_TILE;
+        if ((rc = ws->ensure(1, ntiles, ntiles * stg::TV_STAGE))) return rc;
+        stg::TvLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, d_count, st, fresh, h->num_cu, ev};
+        HIP_TRY(stg::launch_tv(a, ws->d, s));
+    } else {
+        const size_t ntiles = (n + stg::TV_TILE - 1) / stg::TV_TILE;
+        if ((rc = ws->ensure(1, ntiles, 1))) return rc;
+        stg::TopkLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, h->method == M_TOPK, d_count,
+                          h->num_cu, ev};
+        HIP_TRY(stg::launch_topk(a, ws->d, s));
+    }
+    return STG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *stg_last_error(void) { return g_err.c_str(); }
+
+int stg_codec_create(const char *method, int device, stg_codec_t *out) {
+    if (!method || !out) return fail(STG_ERR_INVALID, "null argument");
+    const std::string m(method);
+    auto h = std::make_unique<stg_codec>();
+    if (m == "thresholdv16") { h->method = M_TV16; h->name = "Thresholdv16"; }
+    else if (m == "thresholdv") { h->method = M_TV; h->name = "Thresholdv"; }
+    else if (m == "topk") { h->method = M_TOPK; h->name = "Topk"; }
+    else if (m == "topk_exact") { h->method = M_TOPK_EXACT; h->name = "Topk"; }
+    else return fail(STG_ERR_UNKNOWN, "Unknown compression method " + m + ".");  // core.cpp:117
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(STG_ERR_INVALID, "no such HIP device");
+    h->device = device;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipDeviceGetAttribute(&h->num_cu, hipDeviceAttributeMultiprocessorCount, device));
+    *out = h.release();
+    return STG_OK;
+}
+
+int stg_codec_destroy(stg_codec_t h) {
+    delete h;
+    return STG_OK;
+}
+
+const char *stg_codec_name(stg_codec_t h) { return h ? h->name.c_str() : ""; }
+
+int stg_codec_compress_device(stg_codec_t h, const char *key, const float *d_src, size_t n, uint32_t k,
+                              uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset,
+                              uint32_t *d_count, void *stream) {
+    return run_device(h, key, d_src, d_src, n, k, d_idx, idx_cap, d_val, val_cap, idx_offset, d_count,
+                      static_cast<hipStream_t>(stream));
+}
+
+int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, size_t n, uint32_t k,
+                            uint32_t *dst_idx, size_t idx_cap, float *dst_val, size_t val_cap, int32_t idx_offset,
+                            size_t *out_count) {
+    if (!h || !out_count) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s;
+    int rc = thread_stream(h->device, &s);
+    if (rc) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = h->workspace(s, &ws))) return rc;
+    {
+        std::lock_guard<std::mutex> g(ws->mu);
+        if ((rc = ws->grow(ws->h_src, ws->cap_src, std::max<size_t>(n, 1)))) return rc;
+        size_t co = ws->cap_out;
+        if ((rc = ws->grow(ws->h_idx, co, std::max<size_t>(idx_cap, 1)))) return rc;
+        co = ws->cap_out;
+        if ((rc = ws->grow(ws->h_val, co, std::max<size_t>(idx_cap, 1)))) return rc;
+        ws->cap_out = co;
+        if (!ws->h_count) HIP_TRY(hipMalloc(&ws->h_count, sizeof(uint32_t)));
+        if (!ws->pinned_count) HIP_TRY(hipHostMalloc(&ws->pinned_count, sizeof(uint32_t)));
+        if (n) HIP_TRY(hipMemcpyAsync(ws->h_src, src, n * sizeof(float), hipMemcpyHostToDevice, s));
+    }
+    // threshold-v keys its state by the caller's (host) src pointer
+    rc = run_device(h, key, ws->h_src, src, n, k, ws->h_idx, idx_cap, ws->h_val, idx_cap, idx_offset, ws->h_count, s);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(ws->mu);
+    HIP_TRY(hipMemcpyAsync(ws->pinned_count, ws->h_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (idx_cap) {
+        HIP_TRY(hipMemcpyAsync(dst_idx, ws->h_idx, idx_cap * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(dst_val, ws->h_val, std::min(idx_cap, val_cap) * sizeof(float), hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    *out_count = *ws->pinned_count;
+    return STG_OK;
+}
+
+int stg_codec_get_state(stg_codec_t h, const char *key, const void *key_ptr, float *threshold, float *threshold_inc,
+                        void *stream) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    HIP_TRY(hipSetDevice(h->device));
+    KeyState *st = nullptr;
+    {
+        std::lock_guard<std::mutex> g(h->mu);
+        auto it = h->slot_of.find(state_key(h->method, key, key_ptr));
+        if (it == h->slot_of.end()) return fail(STG_ERR_INVALID, "key has no state yet");
+        st = h->slot_ptr(it->second);
+    }
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    KeyState hs;
+    HIP_TRY(hipMemcpy(&hs, st, sizeof hs, hipMemcpyDeviceToHost));
+    if (threshold) *threshold = hs.t;
+    if (threshold_inc) *threshold_inc = hs.inc;
+    return STG_OK;
+}
+
+int stg_codec_set_timing(stg_codec_t h, int enable) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    std::lock_guard<std::mutex> g(h->mu);
+    h->timing = enable != 0;
+    return STG_OK;
+}
+
+int stg_codec_get_timing(stg_codec_t h, double *ms3, uint64_t *calls) {
+    if (!h || !ms3 || !calls) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    std::lock_guard<std::mutex> g(h->mu);
+    for (auto &e : h->ev_pending) {
+        HIP_TRY(hipEventSynchronize(e[2]));
+        float a = 0, b = 0, c = 0;
+        HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]));
+        HIP_TRY(hipEventElapsedTime(&c, e[0], e[2]));
+        h->ms_acc[0] += a;
+        h->ms_acc[1] += b;
+        h->ms_acc[2] += c;
+        h->timed_calls++;
+        h->ev_pool.push_back(e);
+    }
+    h->ev_pending.clear();
+    for (int i = 0; i < 3; ++i) { ms3[i] = h->ms_acc[i]; h->ms_acc[i] = 0; }
+    *calls = h->timed_calls;
+    h->timed_calls = 0;
+    return STG_OK;
+}
+
+int stg_codec_check(stg_codec_t h) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    HIP_TRY(hipSetDevice(h->device));
+    std::lock_guard<std::mutex> g(h->mu);
+    for (auto &kv : h->ws) {
+        HIP_TRY(hipStreamSynchronize(kv.first));
+        uint32_t f = 0;
+        HIP_TRY(hipMemcpy(&f, kv.second->d.fail, sizeof f, hipMemcpyDeviceToHost));
+        if (f) {
+            char b[96];
+            snprintf(b, sizeof b, "device failure flags 0x%x", f);
+            return fail(STG_ERR_DEVICE, b);
+        }
+    }
+    return STG_OK;
+}
+
+int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t per_rank, int world, size_t n,
+                             float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
+                             uint32_t *d_out_count, void *stream) {
+    if (world < 1) return fail(STG_ERR_INVALID, "world must be >= 1");
+    if (world > 1 && (!d_dense || !d_mark)) return fail(STG_ERR_INVALID, "dense/mark scratch required for world > 1");
+    if (world > 1 && (reinterpret_cast<uintptr_t>(d_mark) & 15u)) return fail(STG_ERR_INVALID, "mark scratch must be 16-byte aligned");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    int ncu = 256;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    static thread_local uint32_t *tiles = nullptr;
+    static thread_local size_t tiles_cap = 0;
+    const size_t need = (n + STG_WG * 16 - 1) / (STG_WG * 16) + 1;
+    if (world > 1 && need > tiles_cap) {
+        HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+        (void)hipFree(tiles);
+        HIP_TRY(hipMalloc(&tiles, need * sizeof(uint32_t)));
+        tiles_cap = need;
+    }
+    HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, n, d_dense, d_mark, d_out_idx, d_out_val,
+                                      d_out_count, tiles, ncu, static_cast<hipStream_t>(stream)));
+    return STG_OK;
+}
+
+int stg_sgd_create(int device, float lr, float momentum, float dampening, float weight_decay, int nesterov,
+                   int maximize, stg_sgd_t *out) {
+    if (!out) return fail(STG_ERR_INVALID, "null argument");
+    auto o = std::make_unique<stg_sgd>();
+    o->device = device;
+    o->lr = lr;
+    o->momentum = momentum;
+    o->dampening = dampening;
+    o->weight_decay = weight_decay;
+    o->nesterov = nesterov != 0;
+    o->maximize = maximize != 0;
+    *out = o.release();
+    return STG_OK;
+}
+
+int stg_sgd_destroy(stg_sgd_t o) {
+    delete o;
+    return STG_OK;
+}
+
+int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len, const float *d_grad,
+                                const uint32_t *d_idx, uint32_t grad_len, const uint32_t *d_grad_len, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    bool first = false;
+    float *mom = nullptr;
+    {
+        std::lock_guard<std::mutex> g(o->mu);
+        if (o->momentum != 0.f) {
+            auto it = o->mom.find(name);
+            if (it == o->mom.end()) {  // sgd.cpp:40-47: zeroed buffer, first = true
+                float *b = nullptr;
+                HIP_TRY(hipMalloc(&b, std::max<size_t>(param_len, 1) * sizeof(float)));
+                HIP_TRY(hipMemsetAsync(b, 0, std::max<size_t>(param_len, 1) * sizeof(float), s));
+                o->mom.emplace(name, std::make_pair(b, param_len));
+                mom = b;
+                first = true;
+            } else {
+                mom = it->second.first;
+            }
+        }
+        o->iter++;  // sgd.cpp:262
+    }
+    stg::SgdLaunch a;
+    a.param = d_param;
+    a.param_len = param_len;
+    a.grad = d_grad;
+    a.gidx = d_idx;
+    a.grad_len = grad_len;
+    a.d_grad_len = d_grad_len;
+    a.mom = mom;
+    a.first = first;
+    a.momentum = o->momentum;
+    a.dampening = o->dampening;
+    a.weight_decay = o->weight_decay;
+    a.lr = o->maximize ? -(double)o->lr : (double)o->lr;  // sgd.cpp:51
+    a.nesterov = o->nesterov;
+    if (grad_len) HIP_TRY(stg::launch_sgd(a, s));
+    return STG_OK;
+}
+
+int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_t len, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    float *b = nullptr;
+    uint32_t n = 0;
+    {
+        std::lock_guard<std::mutex> g(o->mu);
+        auto it = o->mom.find(name);
+        if (it == o->mom.end()) return fail(STG_ERR_INVALID, "no momentum buffer for this name");
+        b = it->second.first;
+        n = it->second.second;
+    }
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    HIP_TRY(hipMemcpy(host_out, b, std::min(len, n) * sizeof(float), hipMemcpyDeviceToHost));
+    return STG_OK;
+}
+
+int stg_synth_fill_device(float *d_dst, size_t n, uint64_t seed, int dist, uint32_t param, void *stream) {
+    if (!n) return STG_OK;
+    HIP_TRY(stg::launch_synth(d_dst, n, seed, dist, param, static_cast<hipStream_t>(stream)));
+    return STG_OK;
+}
+
+}  // extern "C"

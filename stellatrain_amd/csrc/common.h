@@ -1,0 +1,165 @@
+// common.h -- device helpers shared by the codec kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define STG_WG 256           // threads per workgroup (4 waves of 64)
+#define STG_WAVES (STG_WG / 64)
+
+// Per-key AIMD state, one 16-byte slot per key, resident on the device.
+struct KeyState {
+    float t;       // current threshold
+    float inc;     // thresholdv16 additive step (thresholdv16.cpp:96)
+    uint32_t init; // 1 once the first threshold has been computed
+    uint32_t pad;
+};
+
+// Device-side failure bits (read back by stg_codec_check).
+enum : uint32_t {
+    FAIL_SPIN_TIMEOUT = 1u,   // a bounded grid-barrier / arrival spin gave up
+    FAIL_CAND_OVERFLOW = 2u,  // regime-B candidate set exceeded the LDS sort capacity
+    FAIL_LEVELS = 4u,         // regime-B radix descent did not converge
+};
+
+namespace stg {
+
+__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
+
+// Order-preserving float -> uint32 map (for keys that may be negative).
+__device__ __forceinline__ uint32_t ford(float f) {
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// DPP quad permutes (row-local, no LDS traffic).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int QP_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int QP_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave-wide inclusive scan of a uint32 (64 lanes).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
+
+// Workgroup exclusive scan of one uint32 per thread; returns the exclusive
+// prefix and writes the workgroup total to *total.  `sh` needs STG_WAVES+1 words.
+__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t *sh, uint32_t *total) {
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) sh[wave] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) { const uint32_t x = sh[w]; sh[w] = acc; acc += x; }
+        sh[STG_WAVES] = acc;
+    }
+    __syncthreads();
+    const uint32_t r = sh[wave] + inc - v;
+    *total = sh[STG_WAVES];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ uint64_t wg_sum64(uint64_t v, uint64_t *sh) {
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = threadIdx.x >> 6;
+    v = wave_sum64(v);
+    if (lane == 0) sh[wave] = v;
+    __syncthreads();
+    uint64_t t = 0;
+    for (uint32_t w = 0; w < STG_WAVES; ++w) t += sh[w];
+    __syncthreads();
+    return t;
+}
+
+// --- inter-workgroup hand-off (MI355X_MICROARCH "Valid forms", cdna_hip
+//     Guideline 16): producer = every wave drains, barrier, one lane releases
+//     at agent scope then bumps a relaxed agent counter; consumer = one lane
+//     polls relaxed with s_sleep (bounded), one agent acquire, barrier. ---
+__device__ __forceinline__ uint32_t ld_acq_relaxed(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void release_prologue() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// Arrive on a monotonic counter; the caller's lane 0 returns the old value.
+__device__ __forceinline__ uint32_t arrive(uint32_t *ctr) {
+    release_prologue();
+    uint32_t old = 0;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return old;
+}
+
+// Grid barrier on a monotonic counter zeroed before the launch: the b-th
+// barrier (1-based) waits until the counter reaches b * nwg.  Bounded spin.
+__device__ __forceinline__ void grid_barrier(uint32_t *ctr, uint32_t target, uint32_t *fail) {
+    __shared__ uint32_t s_ok;
+    arrive(ctr);
+    if (threadIdx.x == 0) {
+        uint32_t spins = 0;
+        uint32_t ok = 1;
+        while (ld_acq_relaxed(ctr) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 24)) { ok = 0; atomicOr(fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_ok = ok;
+    }
+    __syncthreads();
+    (void)s_ok;
+}
+
+// Wave-aggregated append to a global counter: returns this lane's slot.
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred) {
+    const uint64_t m = __ballot(pred);
+    const uint32_t lane = __lane_id();
+    const uint32_t nb = __popcll(m);
+    const uint32_t leader = m ? (uint32_t)__ffsll((long long)m) - 1u : 0u;
+    uint32_t base = 0;
+    if (m && lane == leader) base = atomicAdd(ctr, nb);
+    base = __shfl(base, (int)leader, 64);
+    const uint32_t below = __popcll(m & ((1ull << lane) - 1ull));
+    return base + below;
+}
+
+}  // namespace stg

@@ -1,0 +1,139 @@
+// ws.h -- per-stream workspace layout shared by host launchers and kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace stg {
+
+constexpr uint32_t TV16_TILE_BLOCKS = 512;   // 16-float lines per scan tile (32 KiB)
+constexpr uint32_t TV16_UNROLL = TV16_TILE_BLOCKS / (STG_WG / 4);  // 8 float4 per lane
+constexpr uint32_t HBINS = 1024;             // regime-B histogram bins per level
+constexpr uint32_t MAX_LEVELS = 6;           // regime-B radix-descent levels
+constexpr uint32_t SORT_CAP = 4096;          // regime-B candidates sortable in LDS
+constexpr uint32_t MAX_FILL_WG = 1024;       // upper bound on fill-kernel workgroups
+
+constexpr uint32_t TV_TILE = 8192;           // threshold-v elements per tile (32 KiB)
+constexpr uint32_t TV_STAGE = 512;           // staged qualifiers per threshold-v tile
+
+constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
+
+// Zeroed at the start of every thresholdv16 call by the scan kernel.
+struct FillCtl {
+    uint32_t bar;       // grid-barrier counter
+    uint32_t arrive;    // last-arriver counter
+    uint32_t cand_n;    // regime-B candidates appended
+    uint32_t pad;
+    uint32_t hist[MAX_LEVELS][HBINS];
+    uint32_t wg_ties[MAX_FILL_WG];
+};
+
+// Per-call scalars handed from the scan kernel to the fill kernel.
+struct CallParams {
+    float t;
+    float inc;
+    uint32_t pad[2];
+};
+
+// Radix-select state (first thresholds, top-k).
+struct RSel {
+    uint32_t prefix;    // bits fixed so far
+    uint32_t mask;      // which bits are fixed
+    uint32_t rank;      // remaining rank (0-based, descending) inside the prefix
+    uint32_t cnt_gt;    // keys strictly above the prefix range
+    uint32_t hist[RS_BINS];
+};
+
+struct DevWS {
+    FillCtl *ctl;
+    CallParams *cp;
+    RSel *rsel;
+    uint32_t *fail;      // sticky failure bits
+    uint64_t *cand;      // regime-B candidates (key << 32 | pos), SORT_CAP entries
+    uint32_t *misc;      // small scratch (counts)
+    float *sums;         // thresholdv16: one sum per 16-float line
+    uint32_t *tile_cnt;  // per-tile qualifier counts
+    uint32_t *tile_aux;  // per-tile secondary counts (threshold-v max, top-k ties)
+    uint32_t *stage_pos; // threshold-v staged positions
+    float *stage_val;    // threshold-v staged values
+};
+
+// ---- launchers (implemented in the .hip files) ----
+struct Tv16Launch {
+    const float *src;
+    size_t n;
+    uint32_t k;
+    uint32_t dst_len;
+    uint32_t *idx;
+    float *val;
+    int32_t idx_offset;
+    uint32_t *count_out;
+    KeyState *state;
+    bool first;
+    int num_cu;
+    hipEvent_t *ev;  // optional [before scan, after scan, after fill]
+};
+hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
+
+struct TvLaunch {
+    const float *src;
+    size_t n;
+    uint32_t k;
+    uint32_t cap;
+    uint32_t *idx;
+    float *val;
+    uint32_t *count_out;
+    KeyState *state;
+    bool first;
+    int num_cu;
+    hipEvent_t *ev;
+};
+hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s);
+
+struct TopkLaunch {
+    const float *src;
+    size_t n;
+    uint32_t k;
+    uint32_t cap;
+    uint32_t *idx;
+    float *val;
+    int32_t idx_offset;
+    bool bug_compat;
+    uint32_t *count_out;
+    int num_cu;
+    hipEvent_t *ev;
+};
+hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s);
+
+// Radix select: the key of descending rank `rank` among (bits(a[i]) & 0x7fffffff),
+// i < m, with the last element's bits additionally masked by `last_mask`, plus
+// `extra_zeros` implicit zero keys.  Result in ws.rsel (prefix = key bits,
+// cnt_gt = keys strictly greater, rank = rank among equal keys).
+hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros,
+                               const uint32_t *d_rank, uint32_t rank, const DevWS &ws, int num_cu,
+                               hipStream_t s);
+
+hipError_t launch_synth(float *dst, size_t n, uint64_t seed, int dist, uint32_t param, hipStream_t s);
+
+hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
+                                float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,
+                                uint32_t *out_count, uint32_t *scratch_tiles, int num_cu, hipStream_t s);
+
+struct SgdLaunch {
+    float *param;
+    uint32_t param_len;
+    const float *grad;
+    const uint32_t *gidx;
+    uint32_t grad_len;
+    const uint32_t *d_grad_len;
+    float *mom;      // momentum buffer (param_len floats) or null when momentum == 0
+    bool first;
+    float momentum, dampening, weight_decay;
+    double lr;
+    bool nesterov;
+};
+hipError_t launch_sgd(const SgdLaunch &a, hipStream_t s);
+
+}  // namespace stg

@@ -1,0 +1,183 @@
+"""The codec-facing surface of ``FasterDpEngine`` and its MERGE call site.
+
+Mirrors (``/root/reference/backend/src``):
+
+* ``FasterDpEngine::configure_compression``        engine/core.cpp:185-195
+* ``FasterDpEngine::configure_compression_ratio``  engine/core.cpp:197-200
+* ``FasterDpEngine::compress(name, tensor, ratio)`` engine/core.cpp:1210-1245
+  (pybind ``fasterdp.compress``, python/pybind.cpp:80-82)
+* ``ModuleCompress::run`` MERGE path                engine/modules/compress.cpp:36-70,139-142,172-186
+* ``ModuleCpuOptimize::run`` MERGE decompress       engine/modules/cpu_optimize.cpp:40-72
+* ``SGD::optimize_raw``                             optim/sgd.cpp:34-263
+
+The rest of the engine (shm, ZMQ ring, scheduler, telemetry) is out of scope
+(SURVEY.md section 2).  All compute runs on the HIP library; this module only
+computes sizes, owns buffers and orders launches on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._capi import CodecError, check, lib
+from .compressor import Compressor, make_compressor
+
+__all__ = ["CodecEngine", "SparseSGD", "merge_numel", "api_numel", "scatter_merge", "owner_of"]
+
+
+def merge_numel(n: int, ratio: float, world: int = 1) -> int:
+    """Pairs per rank on the MERGE path (compress.cpp:44,52): the kept fraction is
+    stored in a float, ``n * k`` is a float product, truncated to int64."""
+    kf = np.float32((1.0 - float(ratio)) / float(np.float32(world)))
+    return max(min(int(n), 1), int(np.float32(np.float32(n) * kf)))
+
+
+def api_numel(n: int, ratio: float) -> int:
+    """``numel_to_select = (1. - ratio) * numel`` with a float ratio (core.cpp:1216)."""
+    return int((1.0 - float(np.float32(ratio))) * n)
+
+
+def owner_of(sizes, world: int) -> list[int]:
+    """Key-affine bucket placement for multi-GPU runs: greedy
+    bytes-balancing in bucket order; a bucket's AIMD state lives on its owner."""
+    load = [0] * world
+    out = []
+    for s in sizes:
+        g = min(range(world), key=lambda r: (load[r], r))
+        load[g] += int(s)
+        out.append(g)
+    return out
+
+
+class CodecEngine:
+    """Codec part of ``FasterDpEngine``: default method thresholdv16
+    (core.cpp:23-26), ratio 0.99, ``compress(name, tensor, ratio)``."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.compression_ratio_ = 0.99
+        self.compressor_: Compressor | None = None
+        self.configure_compression("thresholdv16")
+
+    def configure_compression(self, method: str) -> None:
+        # core.cpp:185-195 accepts only these two; "topk" only via configure()
+        if method not in ("thresholdv", "thresholdv16"):
+            raise CodecError(-2, f"Unknown compression method {method}.")
+        self.compressor_ = make_compressor(method, device=self.device)
+
+    def configure(self, method: str) -> None:
+        """The factory inside FasterDpEngine::configure (core.cpp:110-118)."""
+        self.compressor_ = make_compressor(method, device=self.device)
+
+    def configure_compression_ratio(self, ratio: float) -> None:
+        assert 0 < ratio <= 1
+        self.compression_ratio_ = float(ratio)
+
+    def compression_ratio(self) -> float:
+        return self.compression_ratio_
+
+    def compressor(self) -> Compressor:
+        return self.compressor_
+
+    def compress(self, name: str, tensor, ratio: float):
+        """core.cpp:1210-1245: returns (idx int32, val float32), narrowed to the count."""
+        import torch
+        if ratio < 0 or ratio > 1:
+            raise CodecError(-1, "Ratio must be in range [0, 1].")
+        k = api_numel(tensor.numel(), ratio)
+        dev = tensor.device
+        idx = torch.empty(k, dtype=torch.int32, device=dev)
+        val = torch.empty(k, dtype=torch.float32, device=dev)
+        if k == 0:
+            return idx, val
+        total = self.compressor_.compress(name, tensor.reshape(-1), k, idx, val)
+        if total != k:
+            idx, val = idx.narrow(0, 0, total), val.narrow(0, 0, total)
+        return idx, val
+
+    def compress_bucket(self, key: str, grad, world: int = 1, residual=None):
+        """MERGE path of ModuleCompress::run (compress.cpp:38-70,139-186), device
+        resident and asynchronous.  Returns (idx, val, count) where idx/val have
+        ``numel * world`` zeroed slots (compress.cpp:60-64) and the first
+        ``numel`` are this node's pairs.  With ``residual`` given, applies the
+        error feedback: zero the selected entries of ``grad`` (all ``numel``
+        slots, including unwritten zero indices, compress.cpp:178-179) and copy
+        the bucket into ``residual`` (compress.cpp:185)."""
+        import torch
+        n = grad.numel()
+        numel = merge_numel(n, self.compression_ratio_, world)
+        idx = torch.zeros(numel * world, dtype=torch.int32, device=grad.device)
+        val = torch.zeros(numel * world, dtype=torch.float32, device=grad.device)
+        cnt = self.compressor_.compress_async(key, grad.reshape(-1), numel, idx[:numel], val[:numel], 0)
+        if residual is not None:
+            g = grad.view(-1)
+            g.index_fill_(0, idx[:numel].long(), 0.0)
+            residual.view(-1).copy_(g)
+        return idx, val, cnt
+
+
+def scatter_merge(idx, val, per_rank: int, world: int, n: int, dense=None, mark=None, out_idx=None, out_val=None,
+                  count=None):
+    """MERGE decompress on the device (cpu_optimize.cpp:40-72).  ``dense``
+    (float32[n]) and ``mark`` (uint8[n]) must be zero and are left zero."""
+    import torch
+    dev = idx.device
+    if out_idx is None:
+        out_idx = torch.empty(per_rank * world, dtype=torch.int32, device=dev)
+    if out_val is None:
+        out_val = torch.empty(per_rank * world, dtype=torch.float32, device=dev)
+    if count is None:
+        count = torch.empty(1, dtype=torch.int32, device=dev)
+    if world > 1:
+        if dense is None:
+            dense = torch.zeros(n, dtype=torch.float32, device=dev)
+        if mark is None:
+            mark = torch.zeros(n, dtype=torch.uint8, device=dev)
+    dp = C.c_void_p(dense.data_ptr()) if dense is not None else None
+    mp = C.c_void_p(mark.data_ptr()) if mark is not None else None
+    check(lib().stg_scatter_merge_device(C.c_void_p(idx.data_ptr()), C.c_void_p(val.data_ptr()), per_rank, world, n,
+                                         dp, mp, C.c_void_p(out_idx.data_ptr()), C.c_void_p(out_val.data_ptr()),
+                                         C.c_void_p(count.data_ptr()),
+                                         C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+    return out_idx, out_val, count
+
+
+class SparseSGD:
+    """``SGD`` sparse optimizer (optim/sgd.h:10-50) on the device.  Options as
+    SGD::configure (sgd.cpp:265-300); ``optimize_raw`` as sgd.cpp:34-263."""
+
+    def __init__(self, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                 nesterov: bool = False, maximize: bool = False, device: int = 0):
+        h = C.c_void_p()
+        check(lib().stg_sgd_create(device, lr, momentum, dampening, weight_decay, int(nesterov), int(maximize),
+                                   C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().stg_sgd_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def name(self) -> str:
+        return "SGD"
+
+    def optimize_raw(self, param, name: str, grad, gidx, grad_len: int | None = None, d_grad_len=None) -> None:
+        import torch
+        n = int(grad_len if grad_len is not None else grad.numel())
+        check(lib().stg_sgd_optimize_raw_device(
+            self._h, name.encode(), C.c_void_p(param.data_ptr()), param.numel(), C.c_void_p(grad.data_ptr()),
+            C.c_void_p(gidx.data_ptr()), n, C.c_void_p(d_grad_len.data_ptr()) if d_grad_len is not None else None,
+            C.c_void_p(torch.cuda.current_stream(param.device.index).cuda_stream)))
+
+    def momentum_buffer(self, name: str, n: int):
+        import torch
+        out = np.zeros(n, np.float32)
+        rc = lib().stg_sgd_get_momentum(self._h, name.encode(), C.c_void_p(out.ctypes.data), n,
+                                        C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        return None if rc else out

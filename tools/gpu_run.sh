@@ -1,0 +1,43 @@
+#!/bin/bash
+# GPU-box driver: runs the named steps in order, each under its own time limit,
+# and stops at the first step that ends in anything but success or an ordinary
+# test failure (pytest rc 1).  Logs go to gpurun_out/<step>.log.
+#   tools/gpu_run.sh tests bench breakdown prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+step() {  # name limit cmd...
+    local name=$1 limit=$2
+    shift 2
+    echo "[$(date +%T)] start $name" >> gpurun_out/summary.txt
+    timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $name rc=$rc" >> gpurun_out/summary.txt
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "stopping after $name (rc=$rc)" >> gpurun_out/summary.txt
+        exit $rc
+    fi
+}
+
+for s in "$@"; do
+    case $s in
+        tests) step tests 600 python -m pytest tests -x -q -m gpu ;;
+        tests_all) step tests_all 900 python -m pytest tests -q -m gpu ;;
+        smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+        bench) step bench 400 python bench.py ;;
+        bench_short) step bench_short 300 python bench.py --steps 100 --warmup 16 --cpu-seconds 5 ;;
+        breakdown) step breakdown 300 python tools/breakdown.py ;;
+        breakdown_d3) step breakdown_d3 300 python tools/breakdown.py --dist 2 --param 9000 ;;
+        prof) step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
+                -- python3 bench.py --steps 200 --warmup 32 --no-cpu-baseline ;;
+        pmc_fetch) step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+                -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline ;;
+        pmc_write) step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+                -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline ;;
+        *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
+    esac
+done
+echo "[$(date +%T)] all done" >> gpurun_out/summary.txt
