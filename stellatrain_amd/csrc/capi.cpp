@@ -50,6 +50,7 @@ struct Workspace {
     stg::DevWS d{};
     void *fixed = nullptr;
     size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0;
+    uint32_t epoch = 0;  // thresholdv16 call counter (granule tags)
     // device buffers of the host-memory entry point
     float *h_src = nullptr;
     size_t cap_src = 0;
@@ -269,7 +270,15 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         const size_t nblk = (n + 15) / 16;
         const size_t ntiles = (n / 16 + stg::TV16_TILE_BLOCKS - 1) / stg::TV16_TILE_BLOCKS;
         if ((rc = ws->ensure(nblk, std::max<size_t>(ntiles, 1), 1))) return rc;
-        stg::Tv16Launch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, d_count, st, fresh, h->num_cu, ev};
+        // granule tags are 22-bit (tv16.hip GRAN_EPOCH_MASK): on wrap, clear the
+        // granules so no stale slot can carry the new tag
+        ws->epoch = (ws->epoch + 1) & ((1u << 22) - 1);
+        if (ws->epoch == 0) {
+            ws->epoch = 1;
+            HIP_TRY(hipMemsetAsync(&ws->d.ctl->gran[0], 0, sizeof(ws->d.ctl->gran), s));
+        }
+        stg::Tv16Launch a{d_src,  n,     k,          (uint32_t)idx_cap, d_idx, d_val,    idx_offset,
+                          d_count, st,   fresh,      h->num_cu,         ev,    ws->epoch};
         HIP_TRY(stg::launch_tv16(a, ws->d, s));
     } else if (h->method == M_TV) {
         KeyState *st;

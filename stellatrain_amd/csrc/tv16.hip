@@ -2,7 +2,7 @@
 //
 // Reference: ThresholdvCompressor16::impl_simd_v2
 // (/root/reference/backend/src/compress/thresholdv16.cpp:78-295), first
-// threshold impl_get_first_threshold (:36-54), block sum hsum_float_avx (:57-73).
+// threshold impl_get_first_threshold (:36-54), line sum hsum_float_avx (:57-73).
 //
 // Semantics: walk 16-float lines in index order; a line whose
 // tree-ordered |x| sum S >= t is emitted whole while >= 16 slots remain
@@ -12,17 +12,22 @@
 // lines in descending-sum order (heap fill).  AIMD: t *= 0.99 (in double) when
 // the scan ran dry, t += inc otherwise.
 //
-// GPU structure (two launches per call, first calls add a radix select):
-//   tv16_scan  streaming pass over the bucket: one tree sum per line (a quad of
-//              lanes per line, DPP cross-lane adds in the AVX order), sums to
-//              scratch, per-tile qualifier counts.  HBM-bound: 4n bytes read.
-//   tv16_fill  persistent, one workgroup per CU: global prefix of tile counts,
-//              ordered emission of the first kb(+1) qualifying lines (gathered
-//              from src), stage-3 tail, device-side AIMD update; in regime B a
-//              radix descent over the sums (relative bins just below t, one grid
-//              barrier per level), candidate collection and a last-arriver LDS
-//              sort that orders the heap fill by (sum desc, position asc).
+// One persistent launch per call (tv16_fused), one workgroup per CU, each
+// owning a contiguous range of lines:
+//   1. stream its range once (quad of lanes per line, DPP cross-lane adds in
+//      the AVX tree order), keep the line sums in LDS, count S >= t;
+//   2. publish the count as an epoch-tagged 8-byte granule and gather all
+//      granules (no memset per call, no acquire needed: only atomics cross);
+//   3. every workgroup derives the same regime; emit its qualifying lines
+//      with global rank < kb (+1 partial) straight from src (L2/MALL hot);
+//   4. workgroup 0 writes the stage-3 tail, the AIMD threshold and the count;
+//   5. regime B only: radix descent over the LDS sums (relative bins just
+//      below t, one grid barrier per level), candidate collection, and a
+//      distributed rank-and-emit that orders the heap fill by
+//      (sum desc, position asc).
+// First calls run tv16_seq_sums + radix select (select.hip) before it.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ws.h"
 
@@ -30,7 +35,16 @@ namespace stg {
 
 namespace {
 
-constexpr uint32_t L1_SHIFT = 14;  // level-1 bin width in ulps below t (~0.2% of t)
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t FWG = 1024;        // fused-kernel workgroup: 16 waves, two per CU
+constexpr uint32_t FNW = FWG / 64;
+constexpr uint32_t L1_SHIFT = 14;     // level-1 bin width in ulps below t (~0.2% of t)
+constexpr uint32_t LDS_LINES = SORT_CAP * 2;  // line sums cached in LDS per workgroup
+constexpr uint32_t SCAN_U = 8;        // float4 per lane per batch (two batches in flight)
+constexpr uint32_t MAX_J = LDS_LINES / FWG;
+constexpr uint32_t WIN = 1u << 17;    // regime-B window below t, in ulps (~1.6% of t)
+constexpr uint32_t GRAN_EPOCH_MASK = (1u << 22) - 1;  // granule = epoch:22 | count:21 | window:21
 
 // ---------------------------------------------------------------------------
 // first call: sequential |x| sums per line, last partial line scaled by
@@ -64,83 +78,23 @@ __global__ void tv16_init_state(KeyState *st, const RSel *rs) {
     st->init = 1;
 }
 
-// ---------------------------------------------------------------------------
-// scan: tree sums (AVX order), scratch sums, per-tile qualifier counts
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(STG_WG) tv16_scan(const float *__restrict__ src, uint32_t nb,
-                                                    const KeyState *__restrict__ state, CallParams *cp,
-                                                    float *__restrict__ sums, uint32_t *__restrict__ tile_cnt,
-                                                    FillCtl *ctl, uint32_t nwg_fill) {
-    const float t = state->t;
-    if (blockIdx.x == 0) {
-        // reset the fill kernel's control block for this call
-        uint32_t *z = reinterpret_cast<uint32_t *>(ctl);
-        const uint32_t words = (uint32_t)(offsetof(FillCtl, wg_ties) / 4) + nwg_fill;
-        for (uint32_t i = threadIdx.x; i < words; i += STG_WG) z[i] = 0;
-        if (threadIdx.x == 0) { cp->t = t; cp->inc = state->inc; }
-    }
-    const uint32_t lane = __lane_id();
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t q = lane & 3;
-    const uint32_t tile0 = blockIdx.x * TV16_TILE_BLOCKS;
-
-    float4 v[TV16_UNROLL];
-#pragma unroll
-    for (uint32_t u = 0; u < TV16_UNROLL; ++u) {
-        const uint32_t blk = tile0 + u * (STG_WG / 4) + wave * 16 + (lane >> 2);
-        if (blk < nb) v[u] = *reinterpret_cast<const float4 *>(src + (size_t)blk * 16 + q * 4);
-        else v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    uint32_t cnt = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < TV16_UNROLL; ++u) {
-        const uint32_t blk = tile0 + u * (STG_WG / 4) + wave * 16 + (lane >> 2);
-        const float ax = fabsf(v[u].x), ay = fabsf(v[u].y), az = fabsf(v[u].z), aw = fabsf(v[u].w);
-        // lanes (0,1) hold floats 0..7 of the line, lanes (2,3) floats 8..15:
-        // p = |x_i| + |x_{i+4}| per half, h = (p0+p1)+(p2+p3), S = h_lo + h_hi
-        const float px = ax + dpp_f<QP_XOR1>(ax);
-        const float py = ay + dpp_f<QP_XOR1>(ay);
-        const float pz = az + dpp_f<QP_XOR1>(az);
-        const float pw = aw + dpp_f<QP_XOR1>(aw);
-        const float h = (px + py) + (pz + pw);
-        const float S = h + dpp_f<QP_XOR2>(h);
-        const bool valid = blk < nb;
-        if (valid && q == 0) sums[blk] = S;
-        const bool flag = valid && q == 0 && S >= t;
-        cnt += (uint32_t)__popcll(__ballot(flag));
-    }
-    __shared__ uint32_t s_cnt[STG_WAVES];
-    if (lane == 0) s_cnt[wave] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t c = 0;
-        for (uint32_t w = 0; w < STG_WAVES; ++w) c += s_cnt[w];
-        tile_cnt[blockIdx.x] = c;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// fill
-// ---------------------------------------------------------------------------
-struct FillArgs {
+struct FusedArgs {
     const float *src;
     uint64_t n;
-    uint32_t nb, tl, dst_len, kb, r, ntiles;
+    uint32_t nb, tl, dst_len, kb, r, epoch;
     int32_t idx_offset;
     uint32_t *idx;
     float *val;
     uint32_t *count_out;
     KeyState *state;
-    const CallParams *cp;
-    const float *sums;
-    const uint32_t *tile_cnt;
+    float *sums_g;  // global line sums when a range exceeds LDS_LINES
     FillCtl *ctl;
     uint64_t *cand;
     uint32_t *fail;
 };
 
 template <bool VEC>
-__device__ __forceinline__ void emit_line(const FillArgs &a, uint32_t pos, uint32_t off, uint32_t len) {
+__device__ __forceinline__ void emit_line(const FusedArgs &a, uint32_t pos, uint32_t off, uint32_t len) {
     if (VEC && len == 16) {
         const float4 *s4 = reinterpret_cast<const float4 *>(a.src + pos);
         float4 *v4 = reinterpret_cast<float4 *>(a.val + off);
@@ -162,32 +116,173 @@ __device__ __forceinline__ void emit_line(const FillArgs &a, uint32_t pos, uint3
 
 __device__ __forceinline__ uint32_t bitlen(uint32_t x) { return x ? 32u - __clz(x) : 0u; }
 
-template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
+// Tree sum of one 16-float line held as a float4 by each lane of a quad
+// (lanes 0,1: floats 0..7; lanes 2,3: floats 8..15): p = |x_i| + |x_{i+4}|,
+// h = (p0+p1)+(p2+p3) per half, S = h_lo + h_hi  (thresholdv16.cpp:57-73,143).
+__device__ __forceinline__ float quad_line_sum(const float4 v) {
+    const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z), aw = fabsf(v.w);
+    const float px = ax + dpp_f<QP_XOR1>(ax);
+    const float py = ay + dpp_f<QP_XOR1>(ay);
+    const float pz = az + dpp_f<QP_XOR1>(az);
+    const float pw = aw + dpp_f<QP_XOR1>(aw);
+    const float h = (px + py) + (pz + pw);
+    return h + dpp_f<QP_XOR2>(h);
+}
+
+// STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = return
+// after the streaming pass; 2 = after the count exchange; 3 = plain streaming
+// read (calibration: loads + one add per float4, nothing else).
+template <bool VEC, bool LDS_SUMS, int STAGE = 0>
+__global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
+    __shared__ uint64_t s_buf[SORT_CAP];  // line sums (floats) in 1-5, candidates at the end
     __shared__ uint32_t s_hist[HBINS];
-    __shared__ uint64_t s_sort[SORT_CAP];
-    __shared__ uint32_t sh[STG_WAVES + 1];
-    __shared__ uint64_t sh64[STG_WAVES];
+    __shared__ uint32_t s_wt[MAX_J * FNW + 1];
+    __shared__ uint32_t sh[FNW + 1];
+    __shared__ uint64_t sh64[FNW];
     __shared__ uint32_t s_dec[8];
+    float *s_sum = reinterpret_cast<float *>(s_buf);
+    // STAGE 4 (diagnostics): per-workgroup s_memrealtime (100 MHz) at phase
+    // boundaries into count_out[1 + w*8 + k]
+#define STAMP(k_)                                                                          \
+    do {                                                                                   \
+        if (STAGE == 4 && threadIdx.x == 0)                                                \
+            a.count_out[1 + blockIdx.x * 16 + (k_)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
     const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    const float t = a.cp->t;
-    const float inc = a.cp->inc;
+    const uint32_t lane = __lane_id(), wave = tid >> 6, q = lane & 3;
+    const uint32_t L0 = (uint32_t)((uint64_t)w * a.nb / G);
+    const uint32_t L1 = (uint32_t)((uint64_t)(w + 1) * a.nb / G);
+    const uint32_t nl = L1 - L0;
+    FillCtl *ctl = a.ctl;
+    // Every workgroup reads the state before publishing its count, and
+    // workgroup 0 rewrites it only after it has seen every count.
+    const float t = a.state->t;
+    const float inc = a.state->inc;
     const uint32_t tb = f2u(t);
-    const uint32_t t_begin = (uint32_t)((uint64_t)w * a.ntiles / G);
-    const uint32_t t_end = (uint32_t)((uint64_t)(w + 1) * a.ntiles / G);
+    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;  // window [wlo, tb) just below t
 
-    // ---- phase A: total qualifiers and this workgroup's starting rank ----
-    uint64_t tot = 0, bef = 0;
-    for (uint32_t i = tid; i < a.ntiles; i += STG_WG) {
-        const uint32_t c = a.tile_cnt[i];
-        tot += c;
-        if (i < t_begin) bef += c;
+    if (w == 0) {  // reset this call's control words (write-through) before publishing
+        uint32_t *z = reinterpret_cast<uint32_t *>(ctl);
+        const uint32_t words = (uint32_t)(offsetof(FillCtl, wg_ties) / 4);
+        for (uint32_t i = tid; i < words; i += FWG) st_sc1(z + i, 0u);
     }
-    const uint32_t Qtot = (uint32_t)wg_sum64(tot, sh64);
-    uint32_t P = (uint32_t)wg_sum64(bef, sh64);
 
-    // ---- regime (identical in every workgroup) ----
+    auto put_sum = [&](uint32_t i, float S) {
+        if (LDS_SUMS) s_sum[i] = S;
+        else a.sums_g[L0 + i] = S;
+    };
+    auto get_sum = [&](uint32_t i) -> float { return LDS_SUMS ? s_sum[i] : a.sums_g[L0 + i]; };
+
+    STAMP(0);
+    if (STAGE == 4 && tid == 0) a.count_out[1 + w * 16 + 8] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    // ---- 1. stream the range: line sums, qualifier count, window count ----
+    uint32_t cnt_w = 0, win_w = 0;
+    {
+        const uint32_t lane_line = wave * 16 + (lane >> 2);  // line of this lane in a step
+        constexpr uint32_t STEP = FWG / 4;                   // lines per step
+        const uint32_t nsteps = (nl + STEP - 1) / STEP;
+        const uint32_t nbatch = (nsteps + SCAN_U - 1) / SCAN_U;
+        // One batch of SCAN_U float4 per lane in flight; the 32 waves per CU
+        // (2 workgroups x 16 waves) supply the memory-level parallelism
+        // (tools/ubench_stream.hip: 1 x 1024 threads/CU streams at ~4.0 TB/s,
+        // 2 x 1024 at ~5.4-5.8, nontemporal loads +5%).  Loads are
+        // straight-line: lanes past the range re-read line 0 of the range.
+        for (uint32_t b = 0; b < nbatch; ++b) {
+            float4 v[SCAN_U];
+#pragma unroll
+            for (uint32_t u = 0; u < SCAN_U; ++u) {
+                const uint32_t i = (b * SCAN_U + u) * STEP + lane_line;
+                const uint32_t ic = i < nl ? i : 0u;
+                const f4v t4 = __builtin_nontemporal_load(
+                    reinterpret_cast<const f4v *>(a.src + (size_t)(L0 + ic) * 16 + q * 4));
+                v[u] = make_float4(t4.x, t4.y, t4.z, t4.w);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < SCAN_U; ++u) {
+                const uint32_t i = (b * SCAN_U + u) * STEP + lane_line;
+                if (STAGE == 3) {
+                    cnt_w += f2u(v[u].x + v[u].y + v[u].z + v[u].w) == 0x7f800001u;
+                    continue;
+                }
+                const float S = quad_line_sum(v[u]);
+                const bool lead = i < nl && q == 0;
+                if (lead) put_sum(i, S);
+                const uint32_t us = f2u(S);
+                cnt_w += (uint32_t)__popcll(__ballot(lead && S >= t));
+                win_w += (uint32_t)__popcll(__ballot(lead && us >= wlo && us < tb));
+            }
+        }
+    }
+    if (STAGE == 1 || STAGE == 3) {
+        if (cnt_w == 12345u) a.count_out[1] = win_w;  // keep the loop alive
+        return;
+    }
+    if (lane == 0) { s_wt[wave] = cnt_w; s_wt[FNW + wave] = win_w; }
+    __syncthreads();
+    uint32_t Qw = 0, Ww = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < FNW; ++i) { Qw += s_wt[i]; Ww += s_wt[FNW + i]; }
+    __syncthreads();
+
+    STAMP(1);
+    // ---- 2. publish {epoch, count, window count} as one granule; gather all ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (workgroup 0: the resets above)
+    __syncthreads();
+    const uint64_t tag = (uint64_t)(a.epoch & GRAN_EPOCH_MASK);
+    if (tid == 0) st_sc1(&ctl->gran[w], (tag << 42) | ((uint64_t)Qw << 21) | (uint64_t)Ww);
+    if (wave == 0) {
+        // every slot's load in flight at once; re-poll only the stale ones
+        constexpr uint32_t SL = MAX_FILL_WG / 64;
+        uint64_t g[SL];
+        uint32_t pending = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < SL; ++j) {
+            g[j] = 0;
+            if (j * 64 + lane < G) pending |= 1u << j;
+        }
+        for (uint32_t spins = 0;; ++spins) {
+#pragma unroll
+            for (uint32_t j = 0; j < SL; ++j)
+                if ((pending >> j) & 1u) g[j] = ld_sc1(&ctl->gran[j * 64 + lane]);
+#pragma unroll
+            for (uint32_t j = 0; j < SL; ++j)
+                if (((pending >> j) & 1u) && (g[j] >> 42) == tag) pending &= ~(1u << j);
+            if (!__any(pending != 0)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (spins > (1u << 22)) { atomicOr(a.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+        }
+        uint64_t bef = 0, tot = 0, wbef = 0, wtot = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < SL; ++j) {
+            const uint32_t vv = j * 64 + lane;
+            if (vv < G) {
+                const uint64_t c = (g[j] >> 21) & 0x1FFFFFull, cw = g[j] & 0x1FFFFFull;
+                tot += c;
+                wtot += cw;
+                if (vv < w) { bef += c; wbef += cw; }
+            }
+        }
+        bef = wave_sum64(bef);
+        tot = wave_sum64(tot);
+        wbef = wave_sum64(wbef);
+        wtot = wave_sum64(wtot);
+        if (lane == 0) {
+            s_dec[0] = (uint32_t)bef;
+            s_dec[1] = (uint32_t)tot;
+            s_dec[5] = (uint32_t)wtot;
+            s_dec[6] = (uint32_t)wbef;
+        }
+    }
+    __syncthreads();
+    const uint32_t P = s_dec[0];
+    const uint32_t Qtot = s_dec[1];
+    const uint32_t Wtot = s_dec[5];
+    const uint32_t Wbef = s_dec[6];
+    if (STAGE == 2) return;
+
+    STAMP(2);
+    // ---- 3. regime (identical in every workgroup) ----
     const uint32_t lim = a.kb + (a.r ? 1u : 0u);
     const uint32_t c0 = Qtot >= lim ? a.dst_len : 16u * Qtot;
     bool tail_q = false, tail_cand = false;
@@ -204,48 +299,46 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
     const uint32_t cnt = c0 + ct;
     const bool regimeB = cnt < a.dst_len;
 
-    // ---- phase B: ordered emission of qualifying lines (+ level-1 histogram) ----
-    const uint32_t hi0 = tb - 1u;  // largest candidate key (keys u < tb)
-    if (regimeB) {
-        for (uint32_t i = tid; i < HBINS; i += STG_WG) s_hist[i] = 0;
-        __syncthreads();
-    }
-    constexpr uint32_t PF = 8;  // tiles of sums prefetched per chunk (one latency per chunk)
-    for (uint32_t c0t = t_begin; c0t < t_end; c0t += PF) {
-        if (!regimeB && P >= lim) break;  // uniform: later tiles emit nothing
-        float2 pre[PF];
-#pragma unroll
-        for (uint32_t j = 0; j < PF; ++j) {
-            const uint32_t b0 = (c0t + j) * TV16_TILE_BLOCKS + 2 * tid;
-            pre[j] = make_float2(0.f, 0.f);
-            if (c0t + j < t_end) {
-                if (b0 + 1 < a.nb) pre[j] = *reinterpret_cast<const float2 *>(a.sums + b0);
-                else if (b0 < a.nb) pre[j].x = a.sums[b0];
+    // ---- 3b. ordered emission of this range's qualifying lines ----
+    // line i = j * FWG + tid; in-range rank via ballots (order j, wave, lane)
+    if (P < lim && Qw) {
+        const uint32_t nj = (nl + FWG - 1) / FWG;
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        uint32_t base = P;
+        for (uint32_t j0 = 0; j0 < nj && base < lim; j0 += MAX_J) {
+            const uint32_t jn = std::min(nj - j0, MAX_J);
+            uint32_t flags = 0;
+            for (uint32_t j = 0; j < jn; ++j) {
+                const uint32_t i = (j0 + j) * FWG + tid;
+                const bool f = i < nl && get_sum(i) >= t;
+                flags |= (uint32_t)f << j;
+                const uint64_t bal = __ballot(f);
+                if (lane == 0) s_wt[j * FNW + wave] = (uint32_t)__popcll(bal);
             }
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < PF; ++j) {
-            const uint32_t tile = c0t + j;
-            if (tile >= t_end || (!regimeB && P >= lim)) break;
-            const uint32_t b0 = tile * TV16_TILE_BLOCKS + 2 * tid;
-            const float s0 = pre[j].x, s1 = pre[j].y;
-            const bool v0 = b0 < a.nb, v1 = b0 + 1 < a.nb;
-            const bool f0 = v0 && s0 >= t, f1 = v1 && s1 >= t;
-            uint32_t tcount;
-            const uint32_t ex = wg_excl_scan((uint32_t)f0 + (uint32_t)f1, sh, &tcount);
-            const uint32_t g0 = P + ex, g1 = g0 + (uint32_t)f0;
-            if (f0 && g0 < lim) emit_line<VEC>(a, b0 * 16, 16 * g0, g0 == a.kb ? a.r : 16u);
-            if (f1 && g1 < lim) emit_line<VEC>(a, (b0 + 1) * 16, 16 * g1, g1 == a.kb ? a.r : 16u);
-            if (regimeB) {
-                const uint32_t u0 = f2u(s0), u1 = f2u(s1);
-                if (v0 && !f0 && u0 < tb) atomicAdd(&s_hist[std::min((hi0 - u0) >> L1_SHIFT, HBINS - 1)], 1u);
-                if (v1 && !f1 && u1 < tb) atomicAdd(&s_hist[std::min((hi0 - u1) >> L1_SHIFT, HBINS - 1)], 1u);
+            __syncthreads();
+            if (tid == 0) {
+                uint32_t acc = 0;
+                for (uint32_t i = 0; i < jn * FNW; ++i) { const uint32_t x = s_wt[i]; s_wt[i] = acc; acc += x; }
+                s_wt[MAX_J * FNW] = acc;
             }
-            P += tcount;
+            __syncthreads();
+            for (uint32_t j = 0; j < jn; ++j) {
+                const uint64_t bal = __ballot((flags >> j) & 1u);
+                if ((flags >> j) & 1u) {
+                    const uint32_t g = base + s_wt[j * FNW + wave] + (uint32_t)__popcll(bal & lt);
+                    if (g < lim) {
+                        const uint32_t line = L0 + (j0 + j) * FWG + tid;
+                        emit_line<VEC>(a, line * 16, 16 * g, g == a.kb ? a.r : 16u);
+                    }
+                }
+            }
+            base += s_wt[MAX_J * FNW];  // ranges beyond MAX_J*FWG lines: next chunk
+            __syncthreads();
         }
     }
 
-    // ---- phase C: tail, AIMD, count ----
+    STAMP(3);
+    // ---- 4. tail, AIMD, count (workgroup 0) ----
     if (w == 0 && tid == 0) {
         if (ct) {
             const size_t p0 = (size_t)a.nb * 16;
@@ -261,45 +354,41 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
     }
     if (!regimeB) return;
 
-    // ---- phase D: heap fill = top candidates by (sum desc, position asc) ----
+    // ---- 5. heap fill = top candidates by (sum desc, position asc) ----
     const uint32_t rem = a.dst_len - cnt;
     const uint32_t nc = a.nb - Qtot;  // non-qualifying full lines
     const uint32_t M = std::min((rem + 15u) / 16u, nc);
+    const uint32_t hi0 = tb - 1u;     // largest candidate key (keys u < tb)
     uint32_t nbar = 0;
-    FillCtl *ctl = a.ctl;
 
-    __syncthreads();
-    for (uint32_t i = tid; i < HBINS; i += STG_WG)
-        if (s_hist[i]) atomicAdd(&ctl->hist[0][i], s_hist[i]);
-
-    // mode 1: collect keys >= blo and sort; mode 2: ties at ustar
-    uint32_t mode = 1, blo = tb, ustar = 0, greater = 0, need_eq = 0;
-    if (M > 0) {
-        grid_barrier(&ctl->bar, ++nbar * G, a.fail);
+    // mode 1: collect keys >= blo; mode 2: ties at ustar taken in position order
+    uint32_t mode = 1, blo = tb, ustar = 0, greater = 0;
+    if (M > 0 && Wtot >= M && Wtot + 1 <= SORT_CAP) {
+        blo = wlo;  // the window holds the top M: no histogram needed
+    } else if (M > 0) {
+        for (uint32_t i = tid; i < HBINS; i += FWG) s_hist[i] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < nl; i += FWG) {
+            const uint32_t u = f2u(get_sum(i));
+            if (u < tb) atomicAdd(&s_hist[std::min((hi0 - u) >> L1_SHIFT, HBINS - 1)], 1u);
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < HBINS; i += FWG)
+            if (s_hist[i]) atomicAdd(&ctl->hist[0][i], s_hist[i]);
+        grid_barrier_sc1(&ctl->bar, ++nbar * G, a.fail);
         uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
         bool ovf = true;
         for (;;) {
             // locate the bin holding rank `need` (1-based) counting down from hi
             const uint32_t need = M - above;
-            uint32_t c[HBINS / STG_WG], sum = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < HBINS / STG_WG; ++j) {
-                c[j] = ld_acq_relaxed(&ctl->hist[lvl][tid * (HBINS / STG_WG) + j]);
-                sum += c[j];
-            }
+            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&ctl->hist[lvl][tid]) : 0u;
             uint32_t total;
-            const uint32_t before = wg_excl_scan(sum, sh, &total);
-            if (tid == 0) { s_dec[0] = 0xffffffffu; s_dec[1] = 0; s_dec[2] = 0; }
+            const uint32_t before = blk_excl_scan<FNW>(cbin, sh, &total);
+            if (tid == 0) { s_dec[2] = 0xffffffffu; s_dec[3] = 0; s_dec[4] = 0; }
             __syncthreads();
-            if (need > before && need <= before + sum) {
-                uint32_t acc = before;
-                for (uint32_t j = 0; j < HBINS / STG_WG; ++j) {
-                    if (need <= acc + c[j]) { s_dec[0] = tid * (HBINS / STG_WG) + j; s_dec[1] = acc; s_dec[2] = c[j]; break; }
-                    acc += c[j];
-                }
-            }
+            if (tid < HBINS && need > before && need <= before + cbin) { s_dec[2] = tid; s_dec[3] = before; s_dec[4] = cbin; }
             __syncthreads();
-            const uint32_t bstar = s_dec[0], cum = s_dec[1], hb = s_dec[2];
+            const uint32_t bstar = s_dec[2], cum = s_dec[3], hb = s_dec[4];
             __syncthreads();
             if (bstar == 0xffffffffu) {  // histogram does not reach `need`: collect all
                 if (tid == 0) atomicOr(a.fail, (uint32_t)FAIL_LEVELS);
@@ -309,7 +398,7 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
             if (ovf && bstar == HBINS - 1) {
                 above += cum;
                 const uint64_t width = (uint64_t)(HBINS - 1) << s;
-                if ((uint64_t)hi < width) {  // cannot happen: bin would be empty
+                if ((uint64_t)hi < width) {
                     if (tid == 0) atomicOr(a.fail, (uint32_t)FAIL_LEVELS);
                     mode = 1; blo = 0;
                     break;
@@ -324,7 +413,7 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
                 const uint32_t bl = (uint32_t)std::max<int64_t>((int64_t)lo, blo64);
                 const uint32_t totc = above + cum + hb;
                 if (totc + 1 <= SORT_CAP) { mode = 1; blo = bl; break; }
-                if (s == 0) { mode = 2; ustar = bhi; greater = above + cum; need_eq = need - cum; break; }
+                if (s == 0) { mode = 2; ustar = bhi; greater = above + cum; break; }
                 above += cum;
                 hi = bhi;
                 lo = bl;
@@ -335,66 +424,82 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
                 mode = 1; blo = lo;
                 break;
             }
-            // histogram of this workgroup's candidates inside [lo, hi]
-            for (uint32_t i = tid; i < HBINS; i += STG_WG) s_hist[i] = 0;
+            for (uint32_t i = tid; i < HBINS; i += FWG) s_hist[i] = 0;
             __syncthreads();
-            const uint32_t b_begin = t_begin * TV16_TILE_BLOCKS;
-            const uint32_t b_end = std::min(t_end * TV16_TILE_BLOCKS, a.nb);
-            for (uint32_t b = b_begin + tid; b < b_end; b += STG_WG) {
-                const uint32_t u = f2u(a.sums[b]);
+            for (uint32_t i = tid; i < nl; i += FWG) {
+                const uint32_t u = f2u(get_sum(i));
                 if (u < tb && u >= lo && u <= hi) atomicAdd(&s_hist[(hi - u) >> s], 1u);
             }
             __syncthreads();
-            for (uint32_t i = tid; i < HBINS; i += STG_WG)
+            for (uint32_t i = tid; i < HBINS; i += FWG)
                 if (s_hist[i]) atomicAdd(&ctl->hist[lvl][i], s_hist[i]);
-            grid_barrier(&ctl->bar, ++nbar * G, a.fail);
+            grid_barrier_sc1(&ctl->bar, ++nbar * G, a.fail);
         }
     }
 
-    const uint32_t b_begin = t_begin * TV16_TILE_BLOCKS;
-    const uint32_t b_end = std::min(t_end * TV16_TILE_BLOCKS, a.nb);
+    STAMP(4);
     const uint32_t tailpos = a.nb * 16;
     const bool tail_in_greater = tail_cand && mode == 2 && tail_key > u2f(ustar);
-    // collect: mode 1 -> keys in [blo, tb); mode 2 -> keys in (ustar, tb)
+    // collect (write-through): mode 1 -> keys in [blo, tb); mode 2 -> keys in (ustar, tb).
+    // The window path knows every workgroup's slot range from the exchanged
+    // window counts (no atomics); the rare histogram paths append with one
+    // atomic per workgroup and step.
+    const bool win_path = mode == 1 && blo == wlo && M > 0 && Wtot >= M && Wtot + 1 <= SORT_CAP;
     if (M > 0) {
         const uint32_t kmin = mode == 1 ? blo : ustar + 1;
-        for (uint32_t b0 = b_begin; b0 < b_end; b0 += STG_WG) {
-            const uint32_t b = b0 + tid;
+        uint32_t mine = 0, run = Wbef;
+        for (uint32_t i0 = 0; i0 < nl; i0 += FWG) {
+            const uint32_t i = i0 + tid;
             uint32_t u = 0;
             bool p = false;
-            if (b < b_end) { u = f2u(a.sums[b]); p = u < tb && u >= kmin; }
-            const uint32_t slot = wave_append(&ctl->cand_n, p);
-            if (p && slot < SORT_CAP)
-                a.cand[slot] = ((uint64_t)(~(u | 0x80000000u)) << 32) | (uint64_t)(b * 16);
+            if (i < nl) {
+                u = f2u(get_sum(i));
+                p = u < tb && u >= kmin;
+                mine += mode == 2 && u == ustar;
+            }
+            uint32_t n_here;
+            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, sh, &n_here);
+            if (!n_here) continue;
+            uint32_t base;
+            if (win_path) {
+                base = run;
+                run += n_here;
+            } else {
+                if (tid == 0) s_dec[7] = atomicAdd(&ctl->cand_n, n_here);
+                __syncthreads();
+                base = s_dec[7];
+                __syncthreads();
+            }
+            if (p && base + ex < SORT_CAP)
+                st_sc1(&a.cand[base + ex], ((uint64_t)(~(u | 0x80000000u)) << 32) | (uint64_t)((L0 + i) * 16));
+        }
+        if (mode == 2) {
+            const uint32_t my_ties = (uint32_t)blk_sum64<FNW>(mine, sh64);
+            if (tid == 0) st_sc1(&ctl->wg_ties[w], my_ties);
         }
     }
-    if (mode == 2) {
-        // ties at ustar, taken in position order: per-workgroup counts first
-        uint32_t mine = 0;
-        for (uint32_t b = b_begin + tid; b < b_end; b += STG_WG) mine += f2u(a.sums[b]) == ustar;
-        const uint32_t my_ties = (uint32_t)wg_sum64(mine, sh64);
-        if (tid == 0) ctl->wg_ties[w] = my_ties;
-    }
-    grid_barrier(&ctl->bar, ++nbar * G, a.fail);  // every append / tie count is visible
+    STAMP(5);
+    grid_barrier_sc1(&ctl->bar, ++nbar * G, a.fail);  // every append / tie count is visible
+    STAMP(6);
     if (mode == 2) {
         uint64_t pb = 0, pt = 0;
-        for (uint32_t i = tid; i < G; i += STG_WG) {
+        for (uint32_t i = tid; i < G; i += FWG) {
             const uint32_t x = ld_acq_relaxed(&ctl->wg_ties[i]);
             pt += x;
             if (i < w) pb += x;
         }
-        uint32_t rank = (uint32_t)wg_sum64(pb, sh64);
-        const uint32_t all_ties = (uint32_t)wg_sum64(pt, sh64);
+        uint32_t rank = (uint32_t)blk_sum64<FNW>(pb, sh64);
+        const uint32_t all_ties = (uint32_t)blk_sum64<FNW>(pt, sh64);
         const uint32_t base = cnt + 16u * greater + (tail_in_greater ? a.tl : 0u);
-        for (uint32_t b0 = b_begin; b0 < b_end; b0 += STG_WG) {
-            const uint32_t b = b0 + tid;
-            const bool p = b < b_end && f2u(a.sums[b]) == ustar;
+        for (uint32_t i0 = 0; i0 < nl; i0 += FWG) {
+            const uint32_t i = i0 + tid;
+            const bool p = i < nl && f2u(get_sum(i)) == ustar;
             uint32_t n_here;
-            const uint32_t ex = wg_excl_scan((uint32_t)p, sh, &n_here);
+            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, sh, &n_here);
             if (p) {
                 const uint64_t off = (uint64_t)base + 16ull * (rank + ex);
                 if (off < a.dst_len)
-                    emit_line<VEC>(a, b * 16, (uint32_t)off, std::min<uint32_t>(16u, a.dst_len - (uint32_t)off));
+                    emit_line<VEC>(a, (L0 + i) * 16, (uint32_t)off, std::min<uint32_t>(16u, a.dst_len - (uint32_t)off));
             }
             rank += n_here;
         }
@@ -403,29 +508,30 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
             if (off < a.dst_len)
                 emit_line<false>(a, tailpos, (uint32_t)off, std::min<uint32_t>(a.tl, a.dst_len - (uint32_t)off));
         }
-        (void)need_eq;
+        __syncthreads();  // line sums in s_buf are dead from here on
     }
 
     // ---- distributed rank-and-emit of the collected set ----
     // Output order is (sum desc, position asc) = ascending composite key
     // (~ord(sum) << 32 | pos); an entry's rank is the number of smaller keys,
     // counted by one wave per entry over the LDS copy of the set.
-    uint32_t nc_all = ld_acq_relaxed(&ctl->cand_n);
+    uint32_t nc_all = win_path ? Wtot : ld_acq_relaxed(&ctl->cand_n);
     if (nc_all > SORT_CAP) {
         if (w == 0 && tid == 0) atomicOr(a.fail, (uint32_t)FAIL_CAND_OVERFLOW);
         nc_all = SORT_CAP;
     }
     const bool add_tail = tail_cand && (mode == 1 || tail_in_greater) && nc_all < SORT_CAP;
     const uint32_t total = nc_all + (add_tail ? 1u : 0u);
-    if (w >= total) return;
+    const uint32_t first_e = w * FNW;  // entries handled here: e = w*FNW + wave + k*G*FNW
+    if (first_e >= total) return;
     const uint64_t tail_comp = ((uint64_t)(~ford(tail_key)) << 32) | (uint64_t)tailpos;
-    for (uint32_t i = tid; i < total; i += STG_WG) s_sort[i] = i < nc_all ? a.cand[i] : tail_comp;
     __syncthreads();
-    const uint32_t lane = __lane_id(), wv = tid >> 6;
-    for (uint32_t e = w + G * wv; e < total; e += G * STG_WAVES) {
-        const uint64_t key = s_sort[e];
+    for (uint32_t i = tid; i < total; i += FWG) s_buf[i] = i < nc_all ? ld_sc1(&a.cand[i]) : tail_comp;
+    __syncthreads();
+    for (uint32_t e = first_e + wave; e < total; e += G * FNW) {
+        const uint64_t key = s_buf[e];
         uint32_t less = 0;
-        for (uint32_t j = lane; j < total; j += 64) less += s_sort[j] < key;
+        for (uint32_t j = lane; j < total; j += 64) less += s_buf[j] < key;
         const uint32_t rank = wave_sum(less);
         const bool is_tail = add_tail && key == tail_comp;
         const bool tail_before = add_tail && tail_comp < key;
@@ -440,6 +546,7 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
             }
         }
     }
+    STAMP(7);
 }
 
 }  // namespace
@@ -447,7 +554,6 @@ __global__ void __launch_bounds__(STG_WG) tv16_fill(FillArgs a) {
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     const uint32_t nb = (uint32_t)(a.n / 16);
     const uint32_t tl = (uint32_t)(a.n % 16);
-    const uint32_t ntiles = (nb + TV16_TILE_BLOCKS - 1) / TV16_TILE_BLOCKS;
     if (a.first) {
         const uint32_t nblk = (uint32_t)((a.n + 15) / 16);
         tv16_seq_sums<<<(nblk + STG_WG - 1) / STG_WG, STG_WG, 0, s>>>(a.src, a.n, ws.sums, nblk);
@@ -456,11 +562,13 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         if (e != hipSuccess) return e;
         tv16_init_state<<<1, 1, 0, s>>>(a.state, ws.rsel);
     }
-    const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>((uint32_t)a.num_cu, ntiles), MAX_FILL_WG));
-    if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    tv16_scan<<<std::max<uint32_t>(1, ntiles), STG_WG, 0, s>>>(a.src, nb, a.state, ws.cp, ws.sums, ws.tile_cnt,
-                                                             ws.ctl, G);
-    FillArgs f;
+    // two 1024-thread workgroups per CU (32 waves: full occupancy for the
+    // streaming pass; all co-resident for the in-launch exchanges), at least
+    // 1024 lines (64 KiB) each
+    const uint32_t G = std::max<uint32_t>(
+        1, std::min<uint32_t>(std::min<uint32_t>(2u * (uint32_t)a.num_cu, (nb + 1023) / 1024), MAX_FILL_WG));
+    const uint32_t per = (nb + G - 1) / G;
+    FusedArgs f;
     f.src = a.src;
     f.n = a.n;
     f.nb = nb;
@@ -468,24 +576,33 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     f.dst_len = a.dst_len;
     f.kb = a.dst_len / 16;
     f.r = a.dst_len % 16;
-    f.ntiles = ntiles;
+    f.epoch = a.epoch;
     f.idx_offset = a.idx_offset;
     f.idx = a.idx;
     f.val = a.val;
     f.count_out = a.count_out;
     f.state = a.state;
-    f.cp = ws.cp;
-    f.sums = ws.sums;
-    f.tile_cnt = ws.tile_cnt;
+    f.sums_g = ws.sums;
     f.ctl = ws.ctl;
     f.cand = ws.cand;
     f.fail = ws.fail;
     const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(a.idx) |
                        reinterpret_cast<uintptr_t>(a.val)) & 15u) == 0;
-    if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    if (vec) tv16_fill<true><<<G, STG_WG, 0, s>>>(f);
-    else tv16_fill<false><<<G, STG_WG, 0, s>>>(f);
-    if (a.ev) (void)hipEventRecord(a.ev[2], s);
+    const bool lds = per <= LDS_LINES;
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
+    if (dbg_stage == 1) tv16_fused<true, true, 1><<<G, FWG, 0, s>>>(f);
+    else if (dbg_stage == 2) tv16_fused<true, true, 2><<<G, FWG, 0, s>>>(f);
+    else if (dbg_stage == 3) tv16_fused<true, true, 3><<<G, FWG, 0, s>>>(f);
+    else if (dbg_stage == 4) tv16_fused<true, true, 4><<<G, FWG, 0, s>>>(f);
+    else if (vec && lds) tv16_fused<true, true><<<G, FWG, 0, s>>>(f);
+    else if (vec) tv16_fused<true, false><<<G, FWG, 0, s>>>(f);
+    else if (lds) tv16_fused<false, true><<<G, FWG, 0, s>>>(f);
+    else tv16_fused<false, false><<<G, FWG, 0, s>>>(f);
+    if (a.ev) {
+        (void)hipEventRecord(a.ev[1], s);
+        (void)hipEventRecord(a.ev[2], s);
+    }
     return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ constexpr uint32_t TV16_TILE_BLOCKS = 512;   // 16-float lines per scan tile (32
 constexpr uint32_t TV16_UNROLL = TV16_TILE_BLOCKS / (STG_WG / 4);  // 8 float4 per lane
 constexpr uint32_t HBINS = 1024;             // regime-B histogram bins per level
 constexpr uint32_t MAX_LEVELS = 6;           // regime-B radix-descent levels
-constexpr uint32_t SORT_CAP = 4096;          // regime-B candidates sortable in LDS
+constexpr uint32_t SORT_CAP = 6144;          // regime-B candidates ranked in LDS (48 KiB)
 constexpr uint32_t MAX_FILL_WG = 1024;       // upper bound on fill-kernel workgroups
 
 constexpr uint32_t TV_TILE = 8192;           // threshold-v elements per tile (32 KiB)
@@ -20,14 +20,17 @@ constexpr uint32_t TV_STAGE = 512;           // staged qualifiers per threshold-
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 
-// Zeroed at the start of every thresholdv16 call by the scan kernel.
+// thresholdv16 in-launch control block.  Everything before wg_ties is zeroed
+// by workgroup 0 at the start of every call, before it publishes its count.
 struct FillCtl {
     uint32_t bar;       // grid-barrier counter
-    uint32_t arrive;    // last-arriver counter
+    uint32_t arrive;    // spare arrival counter
     uint32_t cand_n;    // regime-B candidates appended
     uint32_t pad;
     uint32_t hist[MAX_LEVELS][HBINS];
-    uint32_t wg_ties[MAX_FILL_WG];
+    uint32_t wg_ties[MAX_FILL_WG];  // regime-B ties per workgroup (written before read)
+    uint64_t gran[MAX_FILL_WG];     // {epoch, count} granules, epoch-tagged (never zeroed)
+    uint64_t gran2[MAX_FILL_WG];    // {epoch, window count} granules
 };
 
 // Per-call scalars handed from the scan kernel to the fill kernel.
@@ -73,7 +76,8 @@ struct Tv16Launch {
     KeyState *state;
     bool first;
     int num_cu;
-    hipEvent_t *ev;  // optional [before scan, after scan, after fill]
+    hipEvent_t *ev;  // optional [before, mid, after] the codec launch(es)
+    uint32_t epoch;  // per-workspace call counter, never 0 (granule tags)
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
 

@@ -37,6 +37,13 @@ for s in "$@"; do
                 -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline ;;
         pmc_write) step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
                 -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline ;;
+        prof_s1|prof_s2|prof_s3)
+            export STG_DEBUG_TV16_STAGE=${s#prof_s}
+            step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$s" -o run \
+                -- python3 bench.py --steps 200 --warmup 32 --no-cpu-baseline
+            unset STG_DEBUG_TV16_STAGE ;;
+        ubench) step ubench 300 python tools/ubench_read.py ;;
+        stamps) export STG_DEBUG_TV16_STAGE=4; step stamps 300 python tools/stamps.py; unset STG_DEBUG_TV16_STAGE ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
     esac
 done
