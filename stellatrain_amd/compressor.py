@@ -92,6 +92,21 @@ class Compressor:
             int(idx_offset), C.c_void_p(count.data_ptr()), C.c_void_p(_stream_ptr(src.device.index))))
         return count
 
+    def compress_raw(self, key: bytes, src_ptr: int, n: int, k: int, idx_ptr: int, cap: int, val_ptr: int,
+                     count_ptr: int, stream_ptr: int, idx_offset: int = 0) -> None:
+        """Lowest-overhead device call: raw device pointers, no validation
+        beyond the C-ABI's own (for tight host loops such as bench.py)."""
+        rc = self._fn_dev(self._h, key, src_ptr, n, k, idx_ptr, cap, val_ptr, cap, idx_offset, count_ptr, stream_ptr)
+        if rc:
+            check(rc)
+
+    @property
+    def _fn_dev(self):
+        f = getattr(self, "_fn_dev_cache", None)
+        if f is None:
+            f = self._fn_dev_cache = lib().stg_codec_compress_device
+        return f
+
     def _compress_host(self, name, src, k, dst_idx, dst_val, idx_offset) -> int:
         s = src.numpy() if _is_torch(src) else src
         di = dst_idx.numpy() if _is_torch(dst_idx) else dst_idx

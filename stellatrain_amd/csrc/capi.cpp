@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -228,6 +229,28 @@ std::string state_key(Method m, const char *key, const void *src) {
     return key ? std::string(key) : std::string();
 }
 
+// Device-wide admission of fused thresholdv16 kernels.  Each fused launch
+// spin-waits on its own workgroups (count exchange, regime-B barriers), so all
+// of them must be co-resident: with W workgroups per CU at most 2/W fused
+// kernels may be in flight per device.  A launch on stream s first makes s
+// wait for the oldest in-flight fused kernel of another stream when the lane
+// is full (same-stream kernels are already ordered).
+struct FusedLane {
+    std::mutex mu;
+    std::vector<std::pair<hipEvent_t, hipStream_t>> inflight;  // oldest first
+    std::vector<hipEvent_t> pool;
+};
+FusedLane g_lanes[64];
+
+uint32_t fused_wg_per_cu() {
+    static const uint32_t v = [] {
+        const char *e = getenv("STG_TV16_WGPERCU");
+        const int x = e ? atoi(e) : 2;
+        return (uint32_t)(x == 1 ? 1 : 2);
+    }();
+    return v;
+}
+
 thread_local std::unordered_map<int, hipStream_t> t_streams;
 
 int thread_stream(int device, hipStream_t *s) {
@@ -270,16 +293,30 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         const size_t nblk = (n + 15) / 16;
         const size_t ntiles = (n / 16 + stg::TV16_TILE_BLOCKS - 1) / stg::TV16_TILE_BLOCKS;
         if ((rc = ws->ensure(nblk, std::max<size_t>(ntiles, 1), 1))) return rc;
-        // granule tags are 22-bit (tv16.hip GRAN_EPOCH_MASK): on wrap, clear the
-        // granules so no stale slot can carry the new tag
-        ws->epoch = (ws->epoch + 1) & ((1u << 22) - 1);
-        if (ws->epoch == 0) {
+        // 32-bit call epochs tag every hand-off word; epoch parity selects the
+        // per-call counters.  On wrap, clear the whole control block.
+        if (++ws->epoch == 0) {
             ws->epoch = 1;
-            HIP_TRY(hipMemsetAsync(&ws->d.ctl->gran[0], 0, sizeof(ws->d.ctl->gran), s));
+            HIP_TRY(hipMemsetAsync(ws->d.ctl, 0, sizeof(stg::FillCtl), s));
         }
         stg::Tv16Launch a{d_src,  n,     k,          (uint32_t)idx_cap, d_idx, d_val,    idx_offset,
                           d_count, st,   fresh,      h->num_cu,         ev,    ws->epoch};
+        a.wg_per_cu = fused_wg_per_cu();
+        FusedLane &lane = g_lanes[h->device & 63];
+        std::lock_guard<std::mutex> lg(lane.mu);
+        const size_t max_inflight = a.wg_per_cu == 1 ? 2 : 1;
+        while (lane.inflight.size() >= max_inflight) {
+            auto old = lane.inflight.front();
+            lane.inflight.erase(lane.inflight.begin());
+            if (old.second != s) HIP_TRY(hipStreamWaitEvent(s, old.first, 0));
+            lane.pool.push_back(old.first);
+        }
         HIP_TRY(stg::launch_tv16(a, ws->d, s));
+        hipEvent_t done;
+        if (!lane.pool.empty()) { done = lane.pool.back(); lane.pool.pop_back(); }
+        else HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(done, s));
+        lane.inflight.emplace_back(done, s);
     } else if (h->method == M_TV) {
         KeyState *st;
         bool fresh;

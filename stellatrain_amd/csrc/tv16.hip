@@ -44,7 +44,7 @@ constexpr uint32_t LDS_LINES = SORT_CAP * 2;  // line sums cached in LDS per wor
 constexpr uint32_t SCAN_U = 8;        // float4 per lane per batch (two batches in flight)
 constexpr uint32_t MAX_J = LDS_LINES / FWG;
 constexpr uint32_t WIN = 1u << 17;    // regime-B window below t, in ulps (~1.6% of t)
-constexpr uint32_t GRAN_EPOCH_MASK = (1u << 22) - 1;  // granule = epoch:22 | count:21 | window:21
+constexpr uint32_t STAGE_LINES = 256;  // qualifying lines staged in LDS per workgroup (16 KiB)
 
 // ---------------------------------------------------------------------------
 // first call: sequential |x| sums per line, last partial line scaled by
@@ -131,21 +131,23 @@ __device__ __forceinline__ float quad_line_sum(const float4 v) {
 
 // STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = return
 // after the streaming pass; 2 = after the count exchange; 3 = plain streaming
-// read (calibration: loads + one add per float4, nothing else).
+// read (calibration); 4 = full codec + per-workgroup phase stamps.
 template <bool VEC, bool LDS_SUMS, int STAGE = 0>
 __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
     __shared__ uint64_t s_buf[SORT_CAP];  // line sums (floats) in 1-5, candidates at the end
+    __shared__ float4 s_stage[STAGE_LINES * 4];  // qualifying lines, staged during the scan
+    __shared__ uint32_t s_stage_line[STAGE_LINES];
+    __shared__ uint64_t s_mask[MAX_J * FNW];
     __shared__ uint32_t s_hist[HBINS];
     __shared__ uint32_t s_wt[MAX_J * FNW + 1];
     __shared__ uint32_t sh[FNW + 1];
     __shared__ uint64_t sh64[FNW];
     __shared__ uint32_t s_dec[8];
+    __shared__ uint32_t s_nst;
     float *s_sum = reinterpret_cast<float *>(s_buf);
-    // STAGE 4 (diagnostics): per-workgroup s_memrealtime (100 MHz) at phase
-    // boundaries into count_out[1 + w*8 + k]
-#define STAMP(k_)                                                                          \
-    do {                                                                                   \
-        if (STAGE == 4 && threadIdx.x == 0)                                                \
+#define STAMP(k_)                                                                                   \
+    do {                                                                                            \
+        if (STAGE == 4 && threadIdx.x == 0)                                                         \
             a.count_out[1 + blockIdx.x * 16 + (k_)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
@@ -155,34 +157,55 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
     const uint32_t L1 = (uint32_t)((uint64_t)(w + 1) * a.nb / G);
     const uint32_t nl = L1 - L0;
     FillCtl *ctl = a.ctl;
-    // Every workgroup reads the state before publishing its count, and
-    // workgroup 0 rewrites it only after it has seen every count.
+    CallCtl *cc = &ctl->cc[a.epoch & 1u];
+    const uint64_t tag = (uint64_t)a.epoch << 32;
+    // Every workgroup reads the state before it arrives at the count exchange;
+    // workgroup 0 rewrites the state only after the exchange completed.
     const float t = a.state->t;
     const float inc = a.state->inc;
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > WIN ? tb - WIN : 0u;  // window [wlo, tb) just below t
-
-    if (w == 0) {  // reset this call's control words (write-through) before publishing
-        uint32_t *z = reinterpret_cast<uint32_t *>(ctl);
-        const uint32_t words = (uint32_t)(offsetof(FillCtl, wg_ties) / 4);
-        for (uint32_t i = tid; i < words; i += FWG) st_sc1(z + i, 0u);
-    }
 
     auto put_sum = [&](uint32_t i, float S) {
         if (LDS_SUMS) s_sum[i] = S;
         else a.sums_g[L0 + i] = S;
     };
     auto get_sum = [&](uint32_t i) -> float { return LDS_SUMS ? s_sum[i] : a.sums_g[L0 + i]; };
+    // Last-arriver grid barrier, round r (1-based): the workgroup whose arrival
+    // completes the round writes every workgroup's own go word.
+    auto grid_sync = [&](uint32_t r) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) s_dec[7] = __hip_atomic_fetch_add(&cc->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_dec[7] == r * G - 1) {
+            if (tid < G) st_sc1(&ctl->slot[tid].go, tag | r);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        if (tid == 0) {
+            for (uint32_t spins = 0; ld_sc1(&ctl->slot[w].go) != (tag | r); ++spins) {
+                __builtin_amdgcn_s_sleep(1);
+                if (spins > (1u << 24)) { atomicOr(a.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+            }
+        }
+        __syncthreads();
+    };
 
+    if (tid == 0) s_nst = 0;
+    __syncthreads();
     STAMP(0);
     if (STAGE == 4 && tid == 0) a.count_out[1 + w * 16 + 8] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
-    // ---- 1. stream the range: line sums, qualifier count, window count ----
+
+    // ---- 1. stream the range: line sums, qualifier count (+ staging), window count ----
     uint32_t cnt_w = 0, win_w = 0;
     {
         const uint32_t lane_line = wave * 16 + (lane >> 2);  // line of this lane in a step
         constexpr uint32_t STEP = FWG / 4;                   // lines per step
         const uint32_t nsteps = (nl + STEP - 1) / STEP;
         const uint32_t nbatch = (nsteps + SCAN_U - 1) / SCAN_U;
+        const uint32_t leader = lane & ~3u;
+        const uint64_t below_leader = leader ? (~0ull >> (64 - leader)) : 0ull;
         // One batch of SCAN_U float4 per lane in flight; the 32 waves per CU
         // (2 workgroups x 16 waves) supply the memory-level parallelism
         // (tools/ubench_stream.hip: 1 x 1024 threads/CU streams at ~4.0 TB/s,
@@ -209,8 +232,21 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                 const bool lead = i < nl && q == 0;
                 if (lead) put_sum(i, S);
                 const uint32_t us = f2u(S);
-                cnt_w += (uint32_t)__popcll(__ballot(lead && S >= t));
+                const uint64_t bq = __ballot(lead && S >= t);
                 win_w += (uint32_t)__popcll(__ballot(lead && us >= wlo && us < tb));
+                if (bq) {  // stage the qualifying lines (all four lanes of each quad)
+                    cnt_w += (uint32_t)__popcll(bq);
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(&s_nst, (uint32_t)__popcll(bq));
+                    base = __shfl(base, 0, 64);
+                    if ((bq >> leader) & 1ull) {
+                        const uint32_t slot = base + (uint32_t)__popcll(bq & below_leader);
+                        if (slot < STAGE_LINES) {
+                            s_stage[slot * 4 + q] = v[u];
+                            if (q == 0) s_stage_line[slot] = i;
+                        }
+                    }
+                }
             }
         }
     }
@@ -226,30 +262,35 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
     __syncthreads();
 
     STAMP(1);
-    // ---- 2. publish {epoch, count, window count} as one granule; gather all ----
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (workgroup 0: the resets above)
-    __syncthreads();
-    const uint64_t tag = (uint64_t)(a.epoch & GRAN_EPOCH_MASK);
-    if (tid == 0) st_sc1(&ctl->gran[w], (tag << 42) | ((uint64_t)Qw << 21) | (uint64_t)Ww);
+    // ---- 2. count exchange: publish {epoch | count} and {epoch | window count},
+    //         then one wave gathers every workgroup's granules: all slots'
+    //         loads in flight at once, re-polling only the stale ones ----
+    if (tid == 0) {
+        st_sc1(&ctl->gran[w], tag | Qw);
+        st_sc1(&ctl->gran2[w], tag | Ww);
+    }
     if (wave == 0) {
-        // every slot's load in flight at once; re-poll only the stale ones
         constexpr uint32_t SL = MAX_FILL_WG / 64;
-        uint64_t g[SL];
+        uint64_t g[SL], g2[SL];
         uint32_t pending = 0;
 #pragma unroll
         for (uint32_t j = 0; j < SL; ++j) {
-            g[j] = 0;
+            g[j] = g2[j] = 0;
             if (j * 64 + lane < G) pending |= 1u << j;
         }
         for (uint32_t spins = 0;; ++spins) {
 #pragma unroll
             for (uint32_t j = 0; j < SL; ++j)
-                if ((pending >> j) & 1u) g[j] = ld_sc1(&ctl->gran[j * 64 + lane]);
+                if ((pending >> j) & 1u) {
+                    g[j] = ld_sc1(&ctl->gran[j * 64 + lane]);
+                    g2[j] = ld_sc1(&ctl->gran2[j * 64 + lane]);
+                }
 #pragma unroll
             for (uint32_t j = 0; j < SL; ++j)
-                if (((pending >> j) & 1u) && (g[j] >> 42) == tag) pending &= ~(1u << j);
+                if (((pending >> j) & 1u) && (g[j] >> 32) == a.epoch && (g2[j] >> 32) == a.epoch)
+                    pending &= ~(1u << j);
             if (!__any(pending != 0)) break;
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(2);
             if (spins > (1u << 22)) { atomicOr(a.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
         }
         uint64_t bef = 0, tot = 0, wbef = 0, wtot = 0;
@@ -257,7 +298,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
         for (uint32_t j = 0; j < SL; ++j) {
             const uint32_t vv = j * 64 + lane;
             if (vv < G) {
-                const uint64_t c = (g[j] >> 21) & 0x1FFFFFull, cw = g[j] & 0x1FFFFFull;
+                const uint64_t c = (uint32_t)g[j], cw = (uint32_t)g2[j];
                 tot += c;
                 wtot += cw;
                 if (vv < w) { bef += c; wbef += cw; }
@@ -300,45 +341,92 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
     const bool regimeB = cnt < a.dst_len;
 
     // ---- 3b. ordered emission of this range's qualifying lines ----
-    // line i = j * FWG + tid; in-range rank via ballots (order j, wave, lane)
+    // In-range rank of line i = j*FWG + tid via ballot masks (order j, wave, lane).
     if (P < lim && Qw) {
         const uint32_t nj = (nl + FWG - 1) / FWG;
         const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        uint32_t base = P;
-        for (uint32_t j0 = 0; j0 < nj && base < lim; j0 += MAX_J) {
-            const uint32_t jn = std::min(nj - j0, MAX_J);
-            uint32_t flags = 0;
-            for (uint32_t j = 0; j < jn; ++j) {
-                const uint32_t i = (j0 + j) * FWG + tid;
-                const bool f = i < nl && get_sum(i) >= t;
-                flags |= (uint32_t)f << j;
-                const uint64_t bal = __ballot(f);
-                if (lane == 0) s_wt[j * FNW + wave] = (uint32_t)__popcll(bal);
+        if (nj <= MAX_J && Qw <= STAGE_LINES) {
+            // every qualifying line is staged in LDS: one thread per staged line
+            for (uint32_t j = 0; j < nj; ++j) {
+                const uint32_t i = j * FWG + tid;
+                const uint64_t bal = __ballot(i < nl && get_sum(i) >= t);
+                if (lane == 0) { s_mask[j * FNW + wave] = bal; s_wt[j * FNW + wave] = (uint32_t)__popcll(bal); }
             }
             __syncthreads();
             if (tid == 0) {
                 uint32_t acc = 0;
-                for (uint32_t i = 0; i < jn * FNW; ++i) { const uint32_t x = s_wt[i]; s_wt[i] = acc; acc += x; }
-                s_wt[MAX_J * FNW] = acc;
+                for (uint32_t i = 0; i < nj * FNW; ++i) { const uint32_t x = s_wt[i]; s_wt[i] = acc; acc += x; }
             }
             __syncthreads();
-            for (uint32_t j = 0; j < jn; ++j) {
-                const uint64_t bal = __ballot((flags >> j) & 1u);
-                if ((flags >> j) & 1u) {
-                    const uint32_t g = base + s_wt[j * FNW + wave] + (uint32_t)__popcll(bal & lt);
-                    if (g < lim) {
-                        const uint32_t line = L0 + (j0 + j) * FWG + tid;
-                        emit_line<VEC>(a, line * 16, 16 * g, g == a.kb ? a.r : 16u);
+            for (uint32_t e = tid; e < Qw; e += FWG) {
+                const uint32_t i = s_stage_line[e];
+                const uint32_t grp = (i / FWG) * FNW + ((i % FWG) >> 6), ln = i & 63;
+                const uint64_t m = s_mask[grp];
+                const uint32_t g = P + s_wt[grp] + (uint32_t)__popcll(m & (ln ? (~0ull >> (64 - ln)) : 0ull));
+                if (g < lim) {
+                    const uint32_t pos = (L0 + i) * 16;
+                    const uint32_t len = g == a.kb ? a.r : 16u;
+                    const uint32_t off = 16 * g;
+                    if (VEC && len == 16) {
+                        float4 *v4 = reinterpret_cast<float4 *>(a.val + off);
+                        uint4 *i4 = reinterpret_cast<uint4 *>(a.idx + off);
+                        const uint32_t bi = pos + (uint32_t)a.idx_offset;
+#pragma unroll
+                        for (uint32_t c = 0; c < 4; ++c) {
+                            v4[c] = s_stage[e * 4 + c];
+                            i4[c] = make_uint4(bi + 4 * c, bi + 4 * c + 1, bi + 4 * c + 2, bi + 4 * c + 3);
+                        }
+                    } else {
+                        const float *sv = reinterpret_cast<const float *>(&s_stage[e * 4]);
+                        for (uint32_t c = 0; c < len; ++c) {
+                            a.val[off + c] = sv[c];
+                            a.idx[off + c] = pos + c + (uint32_t)a.idx_offset;
+                        }
                     }
                 }
             }
-            base += s_wt[MAX_J * FNW];  // ranges beyond MAX_J*FWG lines: next chunk
-            __syncthreads();
+        } else {
+            // staging overflowed (low threshold): re-read the lines from src
+            uint32_t base = P;
+            for (uint32_t j0 = 0; j0 < nj && base < lim; j0 += MAX_J) {
+                const uint32_t jn = std::min(nj - j0, MAX_J);
+                uint32_t flags = 0;
+                for (uint32_t j = 0; j < jn; ++j) {
+                    const uint32_t i = (j0 + j) * FWG + tid;
+                    const bool f = i < nl && get_sum(i) >= t;
+                    flags |= (uint32_t)f << j;
+                    const uint64_t bal = __ballot(f);
+                    if (lane == 0) s_wt[j * FNW + wave] = (uint32_t)__popcll(bal);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    uint32_t acc = 0;
+                    for (uint32_t i = 0; i < jn * FNW; ++i) { const uint32_t x = s_wt[i]; s_wt[i] = acc; acc += x; }
+                    s_wt[MAX_J * FNW] = acc;
+                }
+                __syncthreads();
+                for (uint32_t j = 0; j < jn; ++j) {
+                    const uint64_t bal = __ballot((flags >> j) & 1u);
+                    if ((flags >> j) & 1u) {
+                        const uint32_t g = base + s_wt[j * FNW + wave] + (uint32_t)__popcll(bal & lt);
+                        if (g < lim) {
+                            const uint32_t line = L0 + (j0 + j) * FWG + tid;
+                            emit_line<VEC>(a, line * 16, 16 * g, g == a.kb ? a.r : 16u);
+                        }
+                    }
+                }
+                base += s_wt[MAX_J * FNW];
+                __syncthreads();
+            }
         }
     }
 
     STAMP(3);
     // ---- 4. tail, AIMD, count (workgroup 0) ----
+    if (w == 0) {  // zero the next call's counters (this call never touches them)
+        uint32_t *z = reinterpret_cast<uint32_t *>(&ctl->cc[(a.epoch + 1) & 1u]);
+        for (uint32_t i = tid; i < sizeof(CallCtl) / 4; i += FWG) st_sc1(z + i, 0u);
+    }
     if (w == 0 && tid == 0) {
         if (ct) {
             const size_t p0 = (size_t)a.nb * 16;
@@ -374,14 +462,14 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
         }
         __syncthreads();
         for (uint32_t i = tid; i < HBINS; i += FWG)
-            if (s_hist[i]) atomicAdd(&ctl->hist[0][i], s_hist[i]);
-        grid_barrier_sc1(&ctl->bar, ++nbar * G, a.fail);
+            if (s_hist[i]) atomicAdd(&cc->hist[0][i], s_hist[i]);
+        grid_sync(++nbar);
         uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
         bool ovf = true;
         for (;;) {
             // locate the bin holding rank `need` (1-based) counting down from hi
             const uint32_t need = M - above;
-            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&ctl->hist[lvl][tid]) : 0u;
+            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&cc->hist[lvl][tid]) : 0u;
             uint32_t total;
             const uint32_t before = blk_excl_scan<FNW>(cbin, sh, &total);
             if (tid == 0) { s_dec[2] = 0xffffffffu; s_dec[3] = 0; s_dec[4] = 0; }
@@ -432,8 +520,8 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
             }
             __syncthreads();
             for (uint32_t i = tid; i < HBINS; i += FWG)
-                if (s_hist[i]) atomicAdd(&ctl->hist[lvl][i], s_hist[i]);
-            grid_barrier_sc1(&ctl->bar, ++nbar * G, a.fail);
+                if (s_hist[i]) atomicAdd(&cc->hist[lvl][i], s_hist[i]);
+            grid_sync(++nbar);
         }
     }
 
@@ -465,7 +553,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                 base = run;
                 run += n_here;
             } else {
-                if (tid == 0) s_dec[7] = atomicAdd(&ctl->cand_n, n_here);
+                if (tid == 0) s_dec[7] = atomicAdd(&cc->cand_n, n_here);
                 __syncthreads();
                 base = s_dec[7];
                 __syncthreads();
@@ -479,7 +567,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
         }
     }
     STAMP(5);
-    grid_barrier_sc1(&ctl->bar, ++nbar * G, a.fail);  // every append / tie count is visible
+    grid_sync(++nbar);  // every append / tie count is visible
     STAMP(6);
     if (mode == 2) {
         uint64_t pb = 0, pt = 0;
@@ -515,7 +603,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
     // Output order is (sum desc, position asc) = ascending composite key
     // (~ord(sum) << 32 | pos); an entry's rank is the number of smaller keys,
     // counted by one wave per entry over the LDS copy of the set.
-    uint32_t nc_all = win_path ? Wtot : ld_acq_relaxed(&ctl->cand_n);
+    uint32_t nc_all = win_path ? Wtot : ld_acq_relaxed(&cc->cand_n);
     if (nc_all > SORT_CAP) {
         if (w == 0 && tid == 0) atomicOr(a.fail, (uint32_t)FAIL_CAND_OVERFLOW);
         nc_all = SORT_CAP;
@@ -547,6 +635,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
         }
     }
     STAMP(7);
+#undef STAMP
 }
 
 }  // namespace
@@ -562,11 +651,11 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         if (e != hipSuccess) return e;
         tv16_init_state<<<1, 1, 0, s>>>(a.state, ws.rsel);
     }
-    // two 1024-thread workgroups per CU (32 waves: full occupancy for the
-    // streaming pass; all co-resident for the in-launch exchanges), at least
-    // 1024 lines (64 KiB) each
+    // wg_per_cu 1024-thread workgroups per CU (2: 32 waves, full occupancy for
+    // one call; 1: half, so two calls from two streams share the CUs), all
+    // co-resident for the in-launch exchanges, at least 1024 lines each
     const uint32_t G = std::max<uint32_t>(
-        1, std::min<uint32_t>(std::min<uint32_t>(2u * (uint32_t)a.num_cu, (nb + 1023) / 1024), MAX_FILL_WG));
+        1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, (nb + 1023) / 1024), MAX_FILL_WG));
     const uint32_t per = (nb + G - 1) / G;
     FusedArgs f;
     f.src = a.src;

@@ -20,17 +20,29 @@ constexpr uint32_t TV_STAGE = 512;           // staged qualifiers per threshold-
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 
-// thresholdv16 in-launch control block.  Everything before wg_ties is zeroed
-// by workgroup 0 at the start of every call, before it publishes its count.
-struct FillCtl {
-    uint32_t bar;       // grid-barrier counter
-    uint32_t arrive;    // spare arrival counter
-    uint32_t cand_n;    // regime-B candidates appended
+// thresholdv16 in-launch control block.
+// Per-call counters come in two copies selected by the call epoch's parity;
+// workgroup 0 zeroes the other copy for the next call (the next call on this
+// workspace is stream-ordered after this kernel).
+struct CallCtl {
+    uint32_t arrive;    // count-exchange arrivals
+    uint32_t bar;       // grid-barrier arrivals (round r completes at r * G)
+    uint32_t cand_n;    // regime-B candidates appended (histogram paths only)
     uint32_t pad;
     uint32_t hist[MAX_LEVELS][HBINS];
+};
+// One 128-byte line per workgroup, written by a barrier's last arriver and
+// polled only by its owner (no line is polled by more than one workgroup).
+struct alignas(128) WgSlot {
+    uint64_t go;        // {epoch:32 | barrier round:32}
+    uint64_t pad[15];
+};
+struct FillCtl {
+    CallCtl cc[2];
     uint32_t wg_ties[MAX_FILL_WG];  // regime-B ties per workgroup (written before read)
-    uint64_t gran[MAX_FILL_WG];     // {epoch, count} granules, epoch-tagged (never zeroed)
-    uint64_t gran2[MAX_FILL_WG];    // {epoch, window count} granules
+    uint64_t gran[MAX_FILL_WG];     // {epoch:32 | count:32}, never zeroed
+    uint64_t gran2[MAX_FILL_WG];    // {epoch:32 | window count:32}
+    WgSlot slot[MAX_FILL_WG];
 };
 
 // Per-call scalars handed from the scan kernel to the fill kernel.
@@ -78,6 +90,7 @@ struct Tv16Launch {
     int num_cu;
     hipEvent_t *ev;  // optional [before, mid, after] the codec launch(es)
     uint32_t epoch;  // per-workspace call counter, never 0 (granule tags)
+    uint32_t wg_per_cu;  // fused-kernel workgroups per CU (1 or 2)
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
 

@@ -43,6 +43,12 @@ for s in "$@"; do
                 -- python3 bench.py --steps 200 --warmup 32 --no-cpu-baseline
             unset STG_DEBUG_TV16_STAGE ;;
         ubench) step ubench 300 python tools/ubench_read.py ;;
+        sweep)
+            for W in 1 2; do for S in 1 2 4; do
+                export STG_TV16_WGPERCU=$W
+                step sweep_w${W}_s${S} 200 python bench.py --steps 400 --warmup 32 --no-cpu-baseline --streams $S
+            done; done
+            unset STG_TV16_WGPERCU ;;
         stamps) export STG_DEBUG_TV16_STAGE=4; step stamps 300 python tools/stamps.py; unset STG_DEBUG_TV16_STAGE ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
     esac
