@@ -1,23 +1,25 @@
 #!/usr/bin/env python3
 """bench.py -- grad-codec GB/s (dense fp32 in) per GPU, thresholdv16 k=1% on 64 MiB buckets.
 
-Workload (BASELINE.json metric): one *step* is one
-thresholdv16 compress call on one 64 MiB fp32 bucket (n = 16,777,216,
-dst_len = 167,772 = merge_numel(n, 0.99)), device resident, through the
-C-ABI.  Each rank owns 8 keys ("<layer>@weight") x 2 alternating buffers
-(the engine's iter%2 shm buffers, core.cpp:967) = 16 distinct buckets
-(1 GiB > 2x the 256 MB Infinity Cache); step s compresses key s%8 from
-buffer (s//8)%2, so every key sees fresh data each visit and the per-key
-AIMD threshold runs its real regime A/B sequence.  Keys are initialised
-(first-threshold call) before the warmup steps.
+Workload (BASELINE.json metric): one *step* is one batched
+thresholdv16 compress over the 8 gradient buckets of one iteration: 8 keys
+("<layer>@weight") x 64 MiB fp32 (n = 16,777,216, dst_len = 167,772 =
+merge_numel(n, 0.99)), device resident, one C-ABI call
+(stg_codec_compress_batch_device) = one persistent kernel launch.  Each rank
+holds 2 buffer sets (the engine's iter%2 shm buffers, core.cpp:967) = 16
+distinct buckets (1 GiB > 2x the 256 MB Infinity Cache); step s compresses
+set s%2, so every key sees fresh data each visit and its AIMD threshold runs
+its real regime A/B sequence.  Keys are initialised (first-threshold call)
+before the warmup steps.  value = 8 x 64 MiB x steps / time.
 
 Multi-GPU: buckets are independent, so each rank compresses its
 own buckets with no collective on the data path ("scaling": "weak");
 value = bytes of all ranks / max-over-ranks time.
 
-Extra fields: ``roofline`` for the dominant kernel (tv16_scan, timed live
-with HIP events on the codec's stream), ``cpu_baseline`` (the oracle port of
-backend/src/compress timed on this host, rank 0 at N=1 only).
+Extra fields: ``roofline`` for the dominant (only) kernel, tv16_batch, timed
+live with HIP events on the codec's stream (algorithmic bytes per launch =
+8 x (4n + 8k)), ``cpu_baseline`` (the oracle port of backend/src/compress
+timed on this host, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -38,15 +40,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=32)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--mib", type=int, default=64)
     p.add_argument("--ratio", type=float, default=0.99)
     p.add_argument("--keys", type=int, default=8)
     p.add_argument("--method", default="thresholdv16")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--profile-steps", type=int, default=64)
+    p.add_argument("--profile-steps", type=int, default=16)
     p.add_argument("--streams", type=int, default=1,
                    help="issue key i's calls on stream i %% S, like the engine's worker pool")
     return p.parse_args()
@@ -74,13 +76,16 @@ def cpu_baseline(n: int, k: int, seconds: float):
                       f"{dt:.1f} s"}
 
 
-def load_traffic():
-    """HBM bytes per tv16_scan launch from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_tv16_scan.json")
+def load_traffic(buckets_per_launch: int):
+    """HBM bytes per tv16_batch launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_tv16_batch.json, written by tools/pmc_summary.py), scaled to
+    this run's buckets per launch."""
+    path = os.path.join(ROOT, "profiles", "pmc_tv16_batch.json")
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get("hbm_bytes_per_launch")
+        d = json.load(open(path))
+        return int(d["hbm_bytes_per_bucket"] * buckets_per_launch)
     except Exception:
         return None
 
@@ -107,9 +112,10 @@ def main():
     n = args.mib * (1 << 20) // 4
     k = merge_numel(n, args.ratio, 1)
     nk = args.keys
+    ns = max(1, min(args.streams, nk))
     comp = make_compressor(args.method, device=local)
     stream = torch.cuda.current_stream(dev)
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
 
     bufs = []
     for b in range(2 * nk):
@@ -117,34 +123,41 @@ def main():
         check(lib().stg_synth_fill_device(C.c_void_p(t.data_ptr()), n, seed_for(rank * 64 + b % nk, b // nk), 0, 0,
                                           C.c_void_p(stream.cuda_stream)))
         bufs.append(t)
-    outs = [(torch.zeros(k, dtype=torch.int32, device=dev), torch.zeros(k, dtype=torch.float32, device=dev),
-             torch.zeros(1, dtype=torch.int32, device=dev)) for _ in range(nk)]
-    keys = [f"{rank * 64 + i}@weight" for i in range(nk)]
+    outs = [(torch.zeros(k, dtype=torch.int32, device=dev), torch.zeros(k, dtype=torch.float32, device=dev))
+            for _ in range(nk)]
+    counts = torch.zeros(nk, dtype=torch.int32, device=dev)
+    keys = [f"{rank * 64 + i}@weight".encode() for i in range(nk)]
 
-    # per-step arguments resolved once: the timed loop is one C-ABI call per step
-    kb = [kk.encode() for kk in keys]
-    sptr = [st.cuda_stream for st in streams]
-    plan = []
-    for s in range(2 * nk):
-        i = s % nk
-        src = bufs[i + nk * ((s // nk) % 2)]
-        oi, ov, oc = outs[i]
-        plan.append((kb[i], src.data_ptr(), n, k, oi.data_ptr(), k, ov.data_ptr(), oc.data_ptr(),
-                     sptr[i % len(streams)]))
+    # Per-step arguments resolved once: a step is one batched C-ABI call per
+    # stream (keys split evenly over the streams), on buffer set s % 2.
+    plans = []
+    for par in range(2):
+        calls = []
+        for j in range(ns):
+            ids = list(range(j, nk, ns))
+            rows = [(keys[i], bufs[i + nk * par].data_ptr(), n, k, outs[i][0].data_ptr(), k, outs[i][1].data_ptr(),
+                     counts.data_ptr() + 4 * i) for i in ids]
+            calls.append((comp.bucket_array(rows), len(rows), streams[j].cuda_stream))
+        plans.append(calls)
 
     def step(s):
-        comp.compress_raw(*plan[s % (2 * nk)])
+        for arr, nb, sp in plans[s % 2]:
+            comp.compress_batch_raw(arr, nb, sp)
+
+    def sync_streams():
+        for st in streams[1:]:
+            stream.wait_stream(st)
+        torch.cuda.synchronize()
 
     # first call per key: first threshold (reported, untimed for the metric)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(nk):
-        step(i)
-    torch.cuda.synchronize()
-    first_ms = (time.perf_counter() - t0) * 1e3 / nk
+    step(0)
+    sync_streams()
+    first_ms = (time.perf_counter() - t0) * 1e3
     for s in range(args.warmup):
-        step(s)
-    torch.cuda.synchronize()
+        step(s + 1)
+    sync_streams()
 
     # ---- timed region ----
     if world > 1:
@@ -154,7 +167,7 @@ def main():
     for s in range(args.steps):
         step(s)
     t_enq = time.perf_counter() - t0
-    torch.cuda.synchronize()
+    sync_streams()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -163,22 +176,24 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt.item())
     comp.check_device()
+    if not os.environ.get("STG_DEBUG_TV16_STAGE"):
+        assert int(counts.min().item()) == k
 
-    # ---- live per-kernel timing (HIP events on the codec's stream) ----
+    # ---- live per-launch timing (HIP events on the codec's stream) ----
     comp.set_timing(True)
     for s in range(args.profile_steps):
         step(s)
-    (scan_ms, fill_ms, call_ms), calls = comp.get_timing()
+    (kern_ms, _fill_ms, call_ms), launches = comp.get_timing()
     comp.set_timing(False)
-    scan_us = scan_ms * 1e3 / max(calls, 1)
-    fill_us = fill_ms * 1e3 / max(calls, 1)
-    call_us = call_ms * 1e3 / max(calls, 1)
+    kern_us = kern_ms * 1e3 / max(launches, 1)
+    per_launch = nk // ns
 
-    total_bytes = 4.0 * n * args.steps * world
+    bucket_bytes = 4.0 * n
+    total_bytes = bucket_bytes * nk * args.steps * world
     value = total_bytes / el / 1e9
     if rank == 0:
-        scan_bytes = 4.0 * n  # algorithmic bytes of the scan kernel: the dense bucket read
-        achieved = scan_bytes / (scan_us * 1e-6) / 1e9
+        alg = per_launch * (4.0 * n + 8.0 * k)  # 4n + 8k per bucket
+        achieved = alg / (kern_us * 1e-6) / 1e9
         out = {
             "metric": "grad-codec GB/s (dense fp32 in) per GPU; thresholdv16 k=1% on 64 MiB bucket",
             "value": round(value, 2),
@@ -191,16 +206,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (splitmix64 Irwin-Hall D1, 16 distinct 64 MiB buckets per GPU, device resident)",
-            "config": {"workload": f"{args.method} k={k} (1%) on {args.mib} MiB fp32 buckets, {nk} keys x 2 buffers",
-                       "streams": args.streams,
+            "data": "synthetic (splitmix64 Irwin-Hall D1, 2 x 8 distinct 64 MiB buckets per GPU, device resident)",
+            "config": {"workload": f"{args.method} k={k} (1%) on {args.mib} MiB fp32 buckets; step = one batched "
+                                   f"call over {nk} keys ({nk * args.mib} MiB)",
+                       "streams": ns, "buckets_per_launch": per_launch,
                        "n": n, "dst_len": k, "parallelism": f"bucket-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(),
-                         "kernel": "tv16_scan", "bytes_per_launch": int(scan_bytes), "avg_us": round(scan_us, 2)},
-            "kernels_us": {"scan": round(scan_us, 2), "fill": round(fill_us, 2), "call": round(call_us, 2),
-                           "first_call_ms": round(first_ms, 3)},
-            "call_gbs_alg": round((4.0 * n + 8.0 * k) / (call_us * 1e-6) / 1e9, 1),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(per_launch),
+                         "kernel": "tv16_batch", "alg_bytes_per_launch": int(alg), "avg_us": round(kern_us, 2)},
+            "per_bucket_us": round(el * 1e6 / (args.steps * nk), 3),
+            "first_call_ms": round(first_ms, 3),
             "host_enqueue_us_per_step": round(t_enq * 1e6 / args.steps, 2),
         }
         if world == 1 and not args.no_cpu_baseline:

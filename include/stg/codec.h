@@ -75,6 +75,29 @@ int stg_codec_compress_device(stg_codec_t h, const char *key, const float *d_src
                               uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap,
                               int32_t idx_offset, uint32_t *d_count, void *stream);
 
+/* One bucket of a batched call: the arguments of one compress_device call. */
+typedef struct stg_bucket {
+    const char *key;
+    const float *d_src;
+    size_t n;
+    uint32_t k;
+    uint32_t *d_idx;
+    size_t idx_cap;
+    float *d_val;
+    size_t val_cap;
+    int32_t idx_offset;
+    uint32_t *d_count;
+} stg_bucket_t;
+
+/* Batched compress_device: same results as calling stg_codec_compress_device
+ * on buckets[0..nbuckets-1] in order on `stream`.  It stands in for the
+ * engine's concurrent MERGE-compress tasks of one iteration (ThreadPool
+ * workers calling compress() on different keys, engine/modules/compress.cpp:
+ * 141, engine/config.h:7).  thresholdv16 runs up to 16 buckets with distinct
+ * keys in one persistent launch, overlapping bucket b's count exchange with
+ * bucket b+1's streaming pass; a repeated key starts a new launch. */
+int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, size_t nbuckets, void *stream);
+
 /* Per-key AIMD state (thresholdv16.cpp:243-259, thresholdv.cpp:72-80), read
  * back for parity tests; synchronises `stream`.  Returns STG_ERR_INVALID when
  * the key has never been compressed.  For threshold-v pass the src pointer
@@ -84,11 +107,15 @@ int stg_codec_get_state(stg_codec_t h, const char *key, const void *key_ptr, flo
 
 /* Kernel timing, the GPU analogue of the reference's CRIT_PATH_compress stat
  * span (engine/modules/compress.cpp:140-142, core_module_api.cpp:504-514):
- * when enabled, every compress records HIP events on its stream around the
- * codec's streaming pass ("scan") and its ordering/emission pass ("fill").
- * stg_codec_get_timing synchronises the recorded events and returns the
- * accumulated milliseconds [scan, fill, whole call] and the number of calls
- * timed, then resets the accumulators. */
+ * when enabled, every codec launch records HIP events on its stream:
+ * [0] = the main kernel (thresholdv16: the whole batch kernel; threshold-v and
+ * top-k: the streaming/count pass), [1] = the ordering/emission pass (0 for
+ * thresholdv16, which has none), [2] = the whole call including first-call
+ * work of threshold-v / top-k (thresholdv16's first-call launches precede
+ * event [0] and are not timed).  stg_codec_get_timing synchronises the recorded events and returns
+ * the accumulated milliseconds [0, 1, 2], the number of launches timed in
+ * *calls and resets the accumulators (one batched call = one launch per run of
+ * distinct keys). */
 int stg_codec_set_timing(stg_codec_t h, int enable);
 int stg_codec_get_timing(stg_codec_t h, double *ms3, uint64_t *calls);
 

@@ -26,6 +26,13 @@ class CodecError(RuntimeError):
         self.code = code
 
 
+class StgBucket(C.Structure):
+    """``stg_bucket_t`` (include/stg/codec.h): one bucket of a batched call."""
+    _fields_ = [("key", C.c_char_p), ("d_src", C.c_void_p), ("n", C.c_size_t), ("k", C.c_uint32),
+                ("d_idx", C.c_void_p), ("idx_cap", C.c_size_t), ("d_val", C.c_void_p), ("val_cap", C.c_size_t),
+                ("idx_offset", C.c_int32), ("d_count", C.c_void_p)]
+
+
 _lib: C.CDLL | None = None
 
 _SIGS = {
@@ -36,6 +43,7 @@ _SIGS = {
                                           C.c_size_t, C.c_void_p, C.c_size_t, C.c_int32, C.POINTER(C.c_size_t)]),
     "stg_codec_compress_device": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p,
                                             C.c_size_t, C.c_void_p, C.c_size_t, C.c_int32, C.c_void_p, C.c_void_p]),
+    "stg_codec_compress_batch_device": (C.c_int, [C.c_void_p, C.POINTER(StgBucket), C.c_size_t, C.c_void_p]),
     "stg_codec_get_state": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.POINTER(C.c_float),
                                       C.POINTER(C.c_float), C.c_void_p]),
     "stg_codec_check": (C.c_int, [C.c_void_p]),

@@ -25,7 +25,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._capi import CodecError, check, lib
+from ._capi import CodecError, StgBucket, check, lib
 
 __all__ = ["Compressor", "ThresholdvCompressor16", "ThresholdvCompressor", "TopkCompressor", "make_compressor",
            "CodecError"]
@@ -97,6 +97,50 @@ class Compressor:
         """Lowest-overhead device call: raw device pointers, no validation
         beyond the C-ABI's own (for tight host loops such as bench.py)."""
         rc = self._fn_dev(self._h, key, src_ptr, n, k, idx_ptr, cap, val_ptr, cap, idx_offset, count_ptr, stream_ptr)
+        if rc:
+            check(rc)
+
+    def compress_batch_async(self, items, stream=None, counts=None):
+        """Batched device compress (``stg_codec_compress_batch_device``): the
+        same results as ``compress_async`` on each (name, src, k, dst_idx,
+        dst_val[, idx_offset]) in order, on one stream.  Returns a
+        (len(items),) int32 tensor of counts (no host sync)."""
+        import torch
+        if not items:
+            return None
+        dev = items[0][1].device
+        if counts is None:
+            counts = torch.zeros(len(items), dtype=torch.int32, device=dev)
+        arr = (StgBucket * len(items))()
+        keep = []
+        for j, it in enumerate(items):
+            name, src, k, di, dv = it[:5]
+            off = it[5] if len(it) > 5 else 0
+            assert src.is_cuda and di.is_cuda and dv.is_cuda and src.dtype == torch.float32
+            assert src.is_contiguous() and di.is_contiguous() and dv.is_contiguous()
+            kb = name.encode()
+            keep.append(kb)
+            arr[j] = StgBucket(kb, src.data_ptr(), src.numel(), int(k), di.data_ptr(), di.numel(), dv.data_ptr(),
+                               dv.numel(), int(off), counts.data_ptr() + 4 * j)
+        sp = stream if stream is not None else _stream_ptr(dev.index)
+        check(lib().stg_codec_compress_batch_device(self._h, arr, len(items), C.c_void_p(sp)))
+        return counts
+
+    @staticmethod
+    def bucket_array(rows):
+        """Prebuilt ``stg_bucket_t`` array from raw tuples (key bytes, src_ptr,
+        n, k, idx_ptr, cap, val_ptr, count_ptr[, idx_offset]) for tight loops."""
+        arr = (StgBucket * len(rows))()
+        for j, r in enumerate(rows):
+            arr[j] = StgBucket(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[5], r[8] if len(r) > 8 else 0, r[7])
+        return arr
+
+    def compress_batch_raw(self, arr, nb: int, stream_ptr: int) -> None:
+        """Batched call on a prebuilt ``bucket_array`` (no per-call marshalling)."""
+        f = getattr(self, "_fn_batch_cache", None)
+        if f is None:
+            f = self._fn_batch_cache = lib().stg_codec_compress_batch_device
+        rc = f(self._h, arr, nb, stream_ptr)
         if rc:
             check(rc)
 

@@ -263,20 +263,117 @@ int thread_stream(int device, hipStream_t *s) {
     return STG_OK;
 }
 
-int run_device(stg_codec *h, const char *key, const float *d_src, const void *key_ptr, size_t n, uint32_t k,
-               uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset, uint32_t *d_count,
-               hipStream_t s) {
-    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+int validate(const stg_codec *h, size_t n, uint32_t k, size_t idx_cap, size_t val_cap, const uint32_t *d_count) {
     if (val_cap < idx_cap) return fail(STG_ERR_INVALID, "value capacity smaller than index capacity");
     if ((h->method == M_TOPK || h->method == M_TOPK_EXACT) && idx_cap < k)
         return fail(STG_ERR_INVALID, "Invalid parameter k");  // topk.cpp:33-34
     if (n >= (size_t(1) << 32) || idx_cap >= (size_t(1) << 32))
         return fail(STG_ERR_UNSUPPORTED, "bucket larger than 2^32-1 elements (uint32 indices)");
     if (!d_count) return fail(STG_ERR_INVALID, "null count pointer");
+    return STG_OK;
+}
+
+// One thresholdv16 launch over `nb` buckets with distinct keys (caller holds
+// ws->mu).  Line-sum scratch is carved per bucket from ws->d.sums.
+int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> &grp, hipStream_t s) {
+    if (grp.empty()) return STG_OK;
+    size_t need = 0;
+    for (auto &b : grp) need += (b.n + 15) / 16 + 64;
+    int rc;
+    if ((rc = ws->ensure(need, 1, 1))) return rc;
+    size_t off = 0;
+    for (auto &b : grp) {
+        b.sums = ws->d.sums + off;
+        off += (b.n + 15) / 16 + 64;
+    }
+    std::array<hipEvent_t, 3> evs{};
+    bool timed = false;
+    if ((rc = h->take_events(&evs, &timed))) return rc;
+    // 24-bit call epochs tag every hand-off word ({epoch:24 | bucket:8});
+    // epoch parity selects the per-call counters.  On wrap, clear the block.
+    if (++ws->epoch >= (1u << 24)) {
+        ws->epoch = 1;
+        HIP_TRY(hipMemsetAsync(ws->d.ctl, 0, sizeof(stg::FillCtl), s));
+    }
+    stg::Tv16Launch a{};
+    a.b = grp.data();
+    a.nb = (uint32_t)grp.size();
+    a.num_cu = h->num_cu;
+    a.ev = timed ? evs.data() : nullptr;
+    a.epoch = ws->epoch;
+    a.wg_per_cu = fused_wg_per_cu();
+    FusedLane &lane = g_lanes[h->device & 63];
+    std::lock_guard<std::mutex> lg(lane.mu);
+    const size_t max_inflight = a.wg_per_cu == 1 ? 2 : 1;
+    while (lane.inflight.size() >= max_inflight) {
+        auto old = lane.inflight.front();
+        lane.inflight.erase(lane.inflight.begin());
+        if (old.second != s) HIP_TRY(hipStreamWaitEvent(s, old.first, 0));
+        lane.pool.push_back(old.first);
+    }
+    HIP_TRY(stg::launch_tv16(a, ws->d, s));
+    hipEvent_t done;
+    if (!lane.pool.empty()) { done = lane.pool.back(); lane.pool.pop_back(); }
+    else HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(done, s));
+    lane.inflight.emplace_back(done, s);
+    grp.clear();
+    return STG_OK;
+}
+
+// thresholdv16 over a sequence of buckets: runs of distinct keys (<= 16)
+// share one launch; the per-key state makes a repeated key wait for the
+// launch that updates it.
+int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s) {
     HIP_TRY(hipSetDevice(h->device));
     Workspace *ws = nullptr;
     int rc = h->workspace(s, &ws);
     if (rc) return rc;
+    std::lock_guard<std::mutex> g(ws->mu);
+    std::vector<stg::Tv16Bucket> grp;
+    grp.reserve(stg::MAX_BATCH);
+    for (size_t i = 0; i < nbk; ++i) {
+        const stg_bucket_t &b = bk[i];
+        if (b.n == 0) {
+            HIP_TRY(hipMemsetAsync(b.d_count, 0, sizeof(uint32_t), s));
+            continue;
+        }
+        KeyState *st;
+        bool fresh;
+        if ((rc = h->slot(state_key(h->method, b.key, b.d_src), &st, &fresh))) return rc;
+        bool dup = false;
+        for (auto &x : grp) dup |= x.state == st;
+        if (dup || grp.size() == stg::MAX_BATCH)
+            if ((rc = launch_tv16_group(h, ws, grp, s))) return rc;
+        stg::Tv16Bucket t{};
+        t.src = b.d_src;
+        t.n = b.n;
+        t.k = b.k;
+        t.dst_len = (uint32_t)b.idx_cap;
+        t.idx = b.d_idx;
+        t.val = b.d_val;
+        t.idx_offset = b.idx_offset;
+        t.count_out = b.d_count;
+        t.state = st;
+        t.first = fresh;
+        grp.push_back(t);
+    }
+    return launch_tv16_group(h, ws, grp, s);
+}
+
+int run_device(stg_codec *h, const char *key, const float *d_src, const void *key_ptr, size_t n, uint32_t k,
+               uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset, uint32_t *d_count,
+               hipStream_t s) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    int rc = validate(h, n, k, idx_cap, val_cap, d_count);
+    if (rc) return rc;
+    if (h->method == M_TV16) {
+        const stg_bucket_t b{key, d_src, n, k, d_idx, idx_cap, d_val, val_cap, idx_offset, d_count};
+        return run_tv16(h, &b, 1, s);
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    Workspace *ws = nullptr;
+    if ((rc = h->workspace(s, &ws))) return rc;
     std::lock_guard<std::mutex> g(ws->mu);
     if (n == 0) {
         HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(uint32_t), s));
@@ -286,38 +383,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
     bool timed = false;
     if ((rc = h->take_events(&evs, &timed))) return rc;
     hipEvent_t *ev = timed ? evs.data() : nullptr;
-    if (h->method == M_TV16) {
-        KeyState *st;
-        bool fresh;
-        if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
-        const size_t nblk = (n + 15) / 16;
-        const size_t ntiles = (n / 16 + stg::TV16_TILE_BLOCKS - 1) / stg::TV16_TILE_BLOCKS;
-        if ((rc = ws->ensure(nblk, std::max<size_t>(ntiles, 1), 1))) return rc;
-        // 32-bit call epochs tag every hand-off word; epoch parity selects the
-        // per-call counters.  On wrap, clear the whole control block.
-        if (++ws->epoch == 0) {
-            ws->epoch = 1;
-            HIP_TRY(hipMemsetAsync(ws->d.ctl, 0, sizeof(stg::FillCtl), s));
-        }
-        stg::Tv16Launch a{d_src,  n,     k,          (uint32_t)idx_cap, d_idx, d_val,    idx_offset,
-                          d_count, st,   fresh,      h->num_cu,         ev,    ws->epoch};
-        a.wg_per_cu = fused_wg_per_cu();
-        FusedLane &lane = g_lanes[h->device & 63];
-        std::lock_guard<std::mutex> lg(lane.mu);
-        const size_t max_inflight = a.wg_per_cu == 1 ? 2 : 1;
-        while (lane.inflight.size() >= max_inflight) {
-            auto old = lane.inflight.front();
-            lane.inflight.erase(lane.inflight.begin());
-            if (old.second != s) HIP_TRY(hipStreamWaitEvent(s, old.first, 0));
-            lane.pool.push_back(old.first);
-        }
-        HIP_TRY(stg::launch_tv16(a, ws->d, s));
-        hipEvent_t done;
-        if (!lane.pool.empty()) { done = lane.pool.back(); lane.pool.pop_back(); }
-        else HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(done, s));
-        lane.inflight.emplace_back(done, s);
-    } else if (h->method == M_TV) {
+    if (h->method == M_TV) {
         KeyState *st;
         bool fresh;
         if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
@@ -372,6 +438,25 @@ int stg_codec_compress_device(stg_codec_t h, const char *key, const float *d_src
                               uint32_t *d_count, void *stream) {
     return run_device(h, key, d_src, d_src, n, k, d_idx, idx_cap, d_val, val_cap, idx_offset, d_count,
                       static_cast<hipStream_t>(stream));
+}
+
+int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, size_t nbuckets, void *stream) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    if (nbuckets && !buckets) return fail(STG_ERR_INVALID, "null bucket array");
+    for (size_t i = 0; i < nbuckets; ++i) {
+        const stg_bucket_t &b = buckets[i];
+        const int rc = validate(h, b.n, b.k, b.idx_cap, b.val_cap, b.d_count);
+        if (rc) return rc;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (h->method == M_TV16) return run_tv16(h, buckets, nbuckets, s);
+    for (size_t i = 0; i < nbuckets; ++i) {
+        const stg_bucket_t &b = buckets[i];
+        const int rc = run_device(h, b.key, b.d_src, b.d_src, b.n, b.k, b.d_idx, b.idx_cap, b.d_val, b.val_cap,
+                                  b.idx_offset, b.d_count, s);
+        if (rc) return rc;
+    }
+    return STG_OK;
 }
 
 int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, size_t n, uint32_t k,

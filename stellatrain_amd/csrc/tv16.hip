@@ -12,20 +12,24 @@
 // lines in descending-sum order (heap fill).  AIMD: t *= 0.99 (in double) when
 // the scan ran dry, t += inc otherwise.
 //
-// One persistent launch per call (tv16_fused), one workgroup per CU, each
-// owning a contiguous range of lines:
-//   1. stream its range once (quad of lanes per line, DPP cross-lane adds in
-//      the AVX tree order), keep the line sums in LDS, count S >= t;
-//   2. publish the count as an epoch-tagged 8-byte granule and gather all
-//      granules (no memset per call, no acquire needed: only atomics cross);
-//   3. every workgroup derives the same regime; emit its qualifying lines
-//      with global rank < kb (+1 partial) straight from src (L2/MALL hot);
-//   4. workgroup 0 writes the stage-3 tail, the AIMD threshold and the count;
-//   5. regime B only: radix descent over the LDS sums (relative bins just
-//      below t, one grid barrier per level), candidate collection, and a
-//      distributed rank-and-emit that orders the heap fill by
-//      (sum desc, position asc).
-// First calls run tv16_seq_sums + radix select (select.hip) before it.
+// One persistent launch per batch of buckets (tv16_batch): 1024-thread
+// workgroups (1 or 2 per CU, all co-resident), each owning a contiguous range
+// of every bucket's lines.  Per bucket b:
+//   scan(b)   stream the range once (a quad of lanes per line, DPP cross-lane
+//             adds in the AVX tree order), keep the line sums in LDS, stage the
+//             qualifying lines' data in LDS, count S >= t and the lines in a
+//             window just below t; publish both counts as tagged granules;
+//   finish(b) gather every workgroup's granules (one wave, all loads in
+//             flight), derive the regime, emit this range's qualifying lines
+//             with global rank < kb (+1 partial) from LDS; workgroup 0 writes
+//             the tail, the AIMD threshold and the count; regime B only: rank
+//             the window candidates (or run a radix descent when the window
+//             does not hold them) with last-arriver grid barriers and emit the
+//             heap fill in (sum desc, position asc) order.
+// The launch runs scan(b+1) before finish(b): bucket b's count exchange and
+// the streaming tail of its slowest workgroups hide behind the next bucket's
+// streaming pass.  A key's first call runs tv16_seq_sums + a radix select
+// (select.hip) before the launch.
 #include <algorithm>
 #include <cstdlib>
 
@@ -35,16 +39,16 @@ namespace stg {
 
 namespace {
 
-typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
-constexpr uint32_t FWG = 1024;        // fused-kernel workgroup: 16 waves, two per CU
+constexpr uint32_t FWG = 1024;     // workgroup: 16 waves
 constexpr uint32_t FNW = FWG / 64;
-constexpr uint32_t L1_SHIFT = 14;     // level-1 bin width in ulps below t (~0.2% of t)
-constexpr uint32_t LDS_LINES = SORT_CAP * 2;  // line sums cached in LDS per workgroup
-constexpr uint32_t SCAN_U = 8;        // float4 per lane per batch (two batches in flight)
-constexpr uint32_t MAX_J = LDS_LINES / FWG;
-constexpr uint32_t WIN = 1u << 17;    // regime-B window below t, in ulps (~1.6% of t)
-constexpr uint32_t STAGE_LINES = 256;  // qualifying lines staged in LDS per workgroup (16 KiB)
+constexpr uint32_t L1_SHIFT = 14;  // level-1 bin width in ulps below t (~0.2% of t)
+constexpr uint32_t LINES_B = 3072; // line sums kept in LDS per workgroup and bucket parity
+constexpr uint32_t STAGE_B = 128;  // qualifying lines staged in LDS per workgroup and parity
+constexpr uint32_t SCAN_U = 8;     // float4 per lane per load batch
+constexpr uint32_t MAX_J = LINES_B / FWG;
+constexpr uint32_t WIN = 1u << 17; // regime-B window below t, in ulps (~1.6% of t)
 
 // ---------------------------------------------------------------------------
 // first call: sequential |x| sums per line, last partial line scaled by
@@ -78,41 +82,52 @@ __global__ void tv16_init_state(KeyState *st, const RSel *rs) {
     st->init = 1;
 }
 
-struct FusedArgs {
+// ---------------------------------------------------------------------------
+// batched persistent kernel
+// ---------------------------------------------------------------------------
+struct BucketDesc {  // 64 bytes
     const float *src;
-    uint64_t n;
-    uint32_t nb, tl, dst_len, kb, r, epoch;
-    int32_t idx_offset;
     uint32_t *idx;
     float *val;
     uint32_t *count_out;
     KeyState *state;
-    float *sums_g;  // global line sums when a range exceeds LDS_LINES
+    float *sums_g;  // line sums of ranges beyond LINES_B
+    uint32_t nb, tl, dst_len;
+    int32_t idx_offset;
+};
+
+struct BatchArgs {
+    BucketDesc bk[MAX_BATCH];
+    uint32_t nbk;
+    uint32_t epoch;  // 1 .. 2^24-1
     FillCtl *ctl;
     uint64_t *cand;
     uint32_t *fail;
+    uint32_t *stamps;  // STAGE 4 diagnostics only
 };
 
-template <bool VEC>
-__device__ __forceinline__ void emit_line(const FusedArgs &a, uint32_t pos, uint32_t off, uint32_t len) {
-    if (VEC && len == 16) {
-        const float4 *s4 = reinterpret_cast<const float4 *>(a.src + pos);
-        float4 *v4 = reinterpret_cast<float4 *>(a.val + off);
-        uint4 *i4 = reinterpret_cast<uint4 *>(a.idx + off);
-        const uint32_t b = pos + (uint32_t)a.idx_offset;
-        const float4 x0 = s4[0], x1 = s4[1], x2 = s4[2], x3 = s4[3];
-        v4[0] = x0; v4[1] = x1; v4[2] = x2; v4[3] = x3;
-        i4[0] = make_uint4(b + 0, b + 1, b + 2, b + 3);
-        i4[1] = make_uint4(b + 4, b + 5, b + 6, b + 7);
-        i4[2] = make_uint4(b + 8, b + 9, b + 10, b + 11);
-        i4[3] = make_uint4(b + 12, b + 13, b + 14, b + 15);
-    } else {
-        for (uint32_t i = 0; i < len; ++i) {
-            a.val[off + i] = a.src[(size_t)pos + i];
-            a.idx[off + i] = pos + i + (uint32_t)a.idx_offset;
-        }
-    }
-}
+// LDS of one workgroup (< 80 KiB: two workgroups per CU).
+struct Lds {
+    float sum[2][LINES_B];          // line sums, by bucket parity
+    float4 stage[2][STAGE_B * 4];   // staged qualifying lines (64 B each)
+    uint32_t stage_line[2][STAGE_B];
+    uint64_t cand[CAND_CAP];        // regime-B candidates (rank phase)
+    uint64_t mask[MAX_J * FNW];
+    uint32_t hist[HBINS];
+    uint32_t wt[MAX_J * FNW + 1];
+    uint32_t sh[FNW + 1];
+    uint64_t sh64[FNW];
+    uint32_t dec[8];
+    uint32_t xch[FNW][4];           // count exchange partials per polling wave
+    uint32_t nst[2];
+    uint32_t cnt[2][2 * FNW];       // per-wave counts of a scan
+};
+
+// Per-bucket values a workgroup carries from scan(b) to finish(b).
+struct Carry {
+    float t, inc;
+    uint32_t qw, ww;  // this range's qualifying / window line counts
+};
 
 __device__ __forceinline__ uint32_t bitlen(uint32_t x) { return x ? 32u - __clz(x) : 0u; }
 
@@ -129,264 +144,335 @@ __device__ __forceinline__ float quad_line_sum(const float4 v) {
     return h + dpp_f<QP_XOR2>(h);
 }
 
-// STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = return
-// after the streaming pass; 2 = after the count exchange; 3 = plain streaming
-// read (calibration); 4 = full codec + per-workgroup phase stamps.
-template <bool VEC, bool LDS_SUMS, int STAGE = 0>
-__global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
-    __shared__ uint64_t s_buf[SORT_CAP];  // line sums (floats) in 1-5, candidates at the end
-    __shared__ float4 s_stage[STAGE_LINES * 4];  // qualifying lines, staged during the scan
-    __shared__ uint32_t s_stage_line[STAGE_LINES];
-    __shared__ uint64_t s_mask[MAX_J * FNW];
-    __shared__ uint32_t s_hist[HBINS];
-    __shared__ uint32_t s_wt[MAX_J * FNW + 1];
-    __shared__ uint32_t sh[FNW + 1];
-    __shared__ uint64_t sh64[FNW];
-    __shared__ uint32_t s_dec[8];
-    __shared__ uint32_t s_nst;
-    float *s_sum = reinterpret_cast<float *>(s_buf);
-#define STAMP(k_)                                                                                   \
-    do {                                                                                            \
-        if (STAGE == 4 && threadIdx.x == 0)                                                         \
-            a.count_out[1 + blockIdx.x * 16 + (k_)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
-    } while (0)
+__device__ __forceinline__ void emit_line(const BucketDesc &d, bool vec, uint32_t pos, uint32_t off, uint32_t len) {
+    if (vec && len == 16) {
+        const float4 *s4 = reinterpret_cast<const float4 *>(d.src + pos);
+        float4 *v4 = reinterpret_cast<float4 *>(d.val + off);
+        uint4 *i4 = reinterpret_cast<uint4 *>(d.idx + off);
+        const uint32_t b = pos + (uint32_t)d.idx_offset;
+        const float4 x0 = s4[0], x1 = s4[1], x2 = s4[2], x3 = s4[3];
+        v4[0] = x0; v4[1] = x1; v4[2] = x2; v4[3] = x3;
+        i4[0] = make_uint4(b + 0, b + 1, b + 2, b + 3);
+        i4[1] = make_uint4(b + 4, b + 5, b + 6, b + 7);
+        i4[2] = make_uint4(b + 8, b + 9, b + 10, b + 11);
+        i4[3] = make_uint4(b + 12, b + 13, b + 14, b + 15);
+    } else {
+        for (uint32_t i = 0; i < len; ++i) {
+            d.val[off + i] = d.src[(size_t)pos + i];
+            d.idx[off + i] = pos + i + (uint32_t)d.idx_offset;
+        }
+    }
+}
 
-    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    const uint32_t lane = __lane_id(), wave = tid >> 6, q = lane & 3;
-    const uint32_t L0 = (uint32_t)((uint64_t)w * a.nb / G);
-    const uint32_t L1 = (uint32_t)((uint64_t)(w + 1) * a.nb / G);
-    const uint32_t nl = L1 - L0;
-    FillCtl *ctl = a.ctl;
-    CallCtl *cc = &ctl->cc[a.epoch & 1u];
-    const uint64_t tag = (uint64_t)a.epoch << 32;
-    // Every workgroup reads the state before it arrives at the count exchange;
-    // workgroup 0 rewrites the state only after the exchange completed.
-    const float t = a.state->t;
-    const float inc = a.state->inc;
-    const uint32_t tb = f2u(t);
-    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;  // window [wlo, tb) just below t
+struct Ctx {
+    const BatchArgs &A;
+    Lds &L;
+    uint32_t G, w, tid, lane, wave;
+    uint32_t nbar;  // grid-barrier rounds used so far (the same in every workgroup)
 
-    auto put_sum = [&](uint32_t i, float S) {
-        if (LDS_SUMS) s_sum[i] = S;
-        else a.sums_g[L0 + i] = S;
-    };
-    auto get_sum = [&](uint32_t i) -> float { return LDS_SUMS ? s_sum[i] : a.sums_g[L0 + i]; };
-    // Last-arriver grid barrier, round r (1-based): the workgroup whose arrival
-    // completes the round writes every workgroup's own go word.
-    auto grid_sync = [&](uint32_t r) {
+    __device__ __forceinline__ uint32_t tag(uint32_t b) const { return (A.epoch << 8) | b; }
+    __device__ __forceinline__ uint32_t range_lo(uint32_t nb) const { return (uint32_t)((uint64_t)w * nb / G); }
+    __device__ __forceinline__ uint32_t range_len(uint32_t nb) const {
+        return (uint32_t)((uint64_t)(w + 1) * nb / G) - range_lo(nb);
+    }
+
+    // Last-arriver grid barrier: the workgroup whose arrival completes round r
+    // writes every workgroup's own go word; each workgroup polls only its own.
+    __device__ __forceinline__ void grid_sync() {
+        const uint32_t r = ++nbar;
+        CallCtl *cc = &A.ctl->cc[A.epoch & 1u];
+        const uint64_t go = ((uint64_t)(A.epoch << 8) << 32) | r;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) s_dec[7] = __hip_atomic_fetch_add(&cc->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) L.dec[7] = __hip_atomic_fetch_add(&cc->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        if (s_dec[7] == r * G - 1) {
-            if (tid < G) st_sc1(&ctl->slot[tid].go, tag | r);
+        if (L.dec[7] == r * G - 1) {
+            for (uint32_t i = tid; i < G; i += FWG) st_sc1(&A.ctl->slot[i].go, go);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
         if (tid == 0) {
-            for (uint32_t spins = 0; ld_sc1(&ctl->slot[w].go) != (tag | r); ++spins) {
+            for (uint32_t spins = 0; ld_sc1(&A.ctl->slot[w].go) != go; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spins > (1u << 24)) { atomicOr(a.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+                if (spins > (1u << 24)) { atomicOr(A.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
             }
         }
         __syncthreads();
-    };
+    }
+};
 
-    if (tid == 0) s_nst = 0;
+// ---- scan(b): stream this workgroup's range of bucket b ----
+template <int STAGE, bool LDS_SUMS>
+__device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b) {
+    const BucketDesc &d = C.A.bk[b];
+    Lds &L = C.L;
+    const uint32_t par = b & 1u;
+    const uint32_t L0 = C.range_lo(d.nb), nl = C.range_len(d.nb);
+    Carry cr;
+    // Read before publishing this bucket's counts: workgroup 0 rewrites the
+    // state only after it has seen every workgroup's counts.
+    cr.t = d.state->t;
+    cr.inc = d.state->inc;
+    const float t = cr.t;
+    const uint32_t tb = f2u(t);
+    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;  // window [wlo, tb) just below t
+    if (C.tid == 0) L.nst[par] = 0;
     __syncthreads();
-    STAMP(0);
-    if (STAGE == 4 && tid == 0) a.count_out[1 + w * 16 + 8] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
 
-    // ---- 1. stream the range: line sums, qualifier count (+ staging), window count ----
+    const uint32_t lane = C.lane, wave = C.wave, q = lane & 3;
+    const uint32_t lane_line = wave * 16 + (lane >> 2);  // line of this lane in a step
+    constexpr uint32_t STEP = FWG / 4;                   // lines per step
+    const uint32_t nbatch = ((nl + STEP - 1) / STEP + SCAN_U - 1) / SCAN_U;
     uint32_t cnt_w = 0, win_w = 0;
-    {
-        const uint32_t lane_line = wave * 16 + (lane >> 2);  // line of this lane in a step
-        constexpr uint32_t STEP = FWG / 4;                   // lines per step
-        const uint32_t nsteps = (nl + STEP - 1) / STEP;
-        const uint32_t nbatch = (nsteps + SCAN_U - 1) / SCAN_U;
-        const uint32_t leader = lane & ~3u;
-        const uint64_t below_leader = leader ? (~0ull >> (64 - leader)) : 0ull;
-        // One batch of SCAN_U float4 per lane in flight; the 32 waves per CU
-        // (2 workgroups x 16 waves) supply the memory-level parallelism
-        // (tools/ubench_stream.hip: 1 x 1024 threads/CU streams at ~4.0 TB/s,
-        // 2 x 1024 at ~5.4-5.8, nontemporal loads +5%).  Loads are
-        // straight-line: lanes past the range re-read line 0 of the range.
-        for (uint32_t b = 0; b < nbatch; ++b) {
-            float4 v[SCAN_U];
+    // One batch of SCAN_U float4 per lane in flight; the 32 waves per CU
+    // supply the memory-level parallelism (tools/ubench_stream.hip: 1 x 1024
+    // threads/CU stream at ~4.0 TB/s, 2 x 1024 at ~5.4-5.8, nontemporal loads
+    // +5%).  Buffer loads (nt) through a descriptor bounded to the range: one
+    // 32-bit voffset per lane, the step in soffset, and lanes past the range
+    // read zeros from the hardware bounds check (no clamping code).
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(d.src + (size_t)L0 * 16), 0, nl * 64u, 0x00020000);
+    const uint32_t voff0 = lane_line * 64u + q * 16u;
+    for (uint32_t bt = 0; bt < nbatch; ++bt) {
+        // opaque per batch: keeps the compiler from hoisting SCAN_U line
+        // indices into live registers across the loop (they would spill)
+        uint32_t ll = lane_line;
+        asm volatile("" : "+v"(ll));
+        float4 v[SCAN_U];
 #pragma unroll
-            for (uint32_t u = 0; u < SCAN_U; ++u) {
-                const uint32_t i = (b * SCAN_U + u) * STEP + lane_line;
-                const uint32_t ic = i < nl ? i : 0u;
-                const f4v t4 = __builtin_nontemporal_load(
-                    reinterpret_cast<const f4v *>(a.src + (size_t)(L0 + ic) * 16 + q * 4));
-                v[u] = make_float4(t4.x, t4.y, t4.z, t4.w);
+        for (uint32_t u = 0; u < SCAN_U; ++u) {
+            const u4v t4 = __builtin_amdgcn_raw_buffer_load_b128(
+                rsrc, voff0, (int)((bt * SCAN_U + u) * STEP * 64u), 2 /* nt */);
+            v[u] = make_float4(__uint_as_float(t4.x), __uint_as_float(t4.y), __uint_as_float(t4.z),
+                               __uint_as_float(t4.w));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < SCAN_U; ++u) {
+            const uint32_t i = (bt * SCAN_U + u) * STEP + ll;
+            if (STAGE == 3) {
+                cnt_w += f2u(v[u].x + v[u].y + v[u].z + v[u].w) == 0x7f800001u;
+                continue;
             }
-#pragma unroll
-            for (uint32_t u = 0; u < SCAN_U; ++u) {
-                const uint32_t i = (b * SCAN_U + u) * STEP + lane_line;
-                if (STAGE == 3) {
-                    cnt_w += f2u(v[u].x + v[u].y + v[u].z + v[u].w) == 0x7f800001u;
-                    continue;
-                }
-                const float S = quad_line_sum(v[u]);
-                const bool lead = i < nl && q == 0;
-                if (lead) put_sum(i, S);
-                const uint32_t us = f2u(S);
-                const uint64_t bq = __ballot(lead && S >= t);
-                win_w += (uint32_t)__popcll(__ballot(lead && us >= wlo && us < tb));
-                if (bq) {  // stage the qualifying lines (all four lanes of each quad)
-                    cnt_w += (uint32_t)__popcll(bq);
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(&s_nst, (uint32_t)__popcll(bq));
-                    base = __shfl(base, 0, 64);
-                    if ((bq >> leader) & 1ull) {
-                        const uint32_t slot = base + (uint32_t)__popcll(bq & below_leader);
-                        if (slot < STAGE_LINES) {
-                            s_stage[slot * 4 + q] = v[u];
-                            if (q == 0) s_stage_line[slot] = i;
-                        }
+            const float S = quad_line_sum(v[u]);  // the same in all four lanes of the quad
+            const bool in = i < nl;
+            if (in && q == 0) {
+                if (LDS_SUMS) L.sum[par][i] = S;
+                else d.sums_g[L0 + i] = S;
+            }
+            const uint32_t us = f2u(S);
+            const bool qual = in && S >= t;
+            const uint64_t bq = __ballot(qual && q == 0);
+            win_w += (uint32_t)__popcll(__ballot(in && q == 0 && us >= wlo && us < tb));
+            if (bq) {  // stage the qualifying lines (all four lanes of each quad)
+                cnt_w += (uint32_t)__popcll(bq);
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&L.nst[par], (uint32_t)__popcll(bq));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (qual) {
+                    // qualifying quads before this one: bq has bits only at quad
+                    // leaders (multiples of 4), so leader p < this leader iff
+                    // p + 3 < lane -- a lane-count of bq << 3 (scalar shift)
+                    const uint64_t b3 = bq << 3;
+                    const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b3, 0u));
+                    if (slot < STAGE_B) {
+                        // lane-in-quad recomputed here (a live copy would spill)
+                        uint32_t lq;
+                        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lq));
+                        lq &= 3u;
+                        L.stage[par][slot * 4 + lq] = v[u];
+                        if (lq == 0) L.stage_line[par][slot] = i;
                     }
                 }
             }
         }
     }
+    if (lane == 0) { L.cnt[par][wave] = cnt_w; L.cnt[par][FNW + wave] = win_w; }
+    __syncthreads();
+    cr.qw = cr.ww = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < FNW; ++i) { cr.qw += L.cnt[par][i]; cr.ww += L.cnt[par][FNW + i]; }
+    // workgroup-uniform: keep the carry in SGPRs across the next scan
+    cr.qw = __builtin_amdgcn_readfirstlane(cr.qw);
+    cr.ww = __builtin_amdgcn_readfirstlane(cr.ww);
     if (STAGE == 1 || STAGE == 3) {
-        if (cnt_w == 12345u) a.count_out[1] = win_w;  // keep the loop alive
-        return;
+        if (cnt_w == 12345u) d.count_out[1] = win_w;  // keep the loop alive
+        return cr;
     }
-    if (lane == 0) { s_wt[wave] = cnt_w; s_wt[FNW + wave] = win_w; }
-    __syncthreads();
-    uint32_t Qw = 0, Ww = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < FNW; ++i) { Qw += s_wt[i]; Ww += s_wt[FNW + i]; }
-    __syncthreads();
+    if (C.tid == 0) {
+        const uint64_t tg = (uint64_t)C.tag(b) << 32;
+        st_sc1(&C.A.ctl->gran[b][C.w], tg | cr.qw);
+        st_sc1(&C.A.ctl->gran2[b][C.w], tg | cr.ww);
+    }
+    return cr;
+}
 
-    STAMP(1);
-    // ---- 2. count exchange: publish {epoch | count} and {epoch | window count},
-    //         then one wave gathers every workgroup's granules: all slots'
-    //         loads in flight at once, re-polling only the stale ones ----
-    if (tid == 0) {
-        st_sc1(&ctl->gran[w], tag | Qw);
-        st_sc1(&ctl->gran2[w], tag | Ww);
-    }
-    if (wave == 0) {
-        constexpr uint32_t SL = MAX_FILL_WG / 64;
-        uint64_t g[SL], g2[SL];
-        uint32_t pending = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < SL; ++j) {
-            g[j] = g2[j] = 0;
-            if (j * 64 + lane < G) pending |= 1u << j;
-        }
-        for (uint32_t spins = 0;; ++spins) {
-#pragma unroll
-            for (uint32_t j = 0; j < SL; ++j)
-                if ((pending >> j) & 1u) {
-                    g[j] = ld_sc1(&ctl->gran[j * 64 + lane]);
-                    g2[j] = ld_sc1(&ctl->gran2[j * 64 + lane]);
-                }
-#pragma unroll
-            for (uint32_t j = 0; j < SL; ++j)
-                if (((pending >> j) & 1u) && (g[j] >> 32) == a.epoch && (g2[j] >> 32) == a.epoch)
-                    pending &= ~(1u << j);
-            if (!__any(pending != 0)) break;
-            __builtin_amdgcn_s_sleep(2);
-            if (spins > (1u << 22)) { atomicOr(a.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
-        }
-        uint64_t bef = 0, tot = 0, wbef = 0, wtot = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < SL; ++j) {
-            const uint32_t vv = j * 64 + lane;
-            if (vv < G) {
-                const uint64_t c = (uint32_t)g[j], cw = (uint32_t)g2[j];
-                tot += c;
-                wtot += cw;
-                if (vv < w) { bef += c; wbef += cw; }
+// Mode-1 / mode-2 follow-up state of a regime-B bucket.
+struct Defer {
+    uint32_t active, b, cnt;
+    uint32_t nc;         // candidate count (window path) or ~0 = read cand_n
+    uint32_t tail_cand;  // the ragged tail competes in the heap fill
+    float tail_key;
+};
+
+// Distributed rank-and-emit of a collected candidate set: output order is
+// (sum desc, position asc) = ascending composite key (~ord(sum) << 32 | pos);
+// an entry's rank is the number of smaller keys, counted by one wave per
+// entry over the LDS copy of the set (+ the ragged tail when it competes).
+__device__ __forceinline__ void rank_emit(Ctx &C, const BucketDesc &d, const uint64_t *cand, uint32_t cnt,
+                                          uint32_t nc_all, bool add_tail, float tail_key) {
+    Lds &L = C.L;
+    const uint32_t total = nc_all + (add_tail ? 1u : 0u);
+    const uint32_t first_e = C.w * FNW;  // entries handled here: e = w*FNW + wave + k*G*FNW
+    if (first_e >= total) return;
+    const uint32_t tailpos = d.nb * 16;
+    const uint64_t tail_comp = ((uint64_t)(~ford(tail_key)) << 32) | (uint64_t)tailpos;
+    for (uint32_t i = C.tid; i < total; i += FWG) L.cand[i] = i < nc_all ? ld_sc1(&cand[i]) : tail_comp;
+    __syncthreads();
+    for (uint32_t e = first_e + C.wave; e < total; e += C.G * FNW) {
+        const uint64_t key = L.cand[e];
+        uint32_t less = 0;
+        for (uint32_t j = C.lane; j < total; j += 64) less += L.cand[j] < key;
+        const uint32_t rank = wave_sum(less);
+        const bool is_tail = add_tail && key == tail_comp;
+        const bool tail_before = add_tail && tail_comp < key;
+        const uint32_t pos = (uint32_t)key;
+        const uint32_t len = is_tail ? d.tl : 16u;
+        const uint64_t off = (uint64_t)cnt + 16ull * rank - (tail_before ? (uint64_t)(16u - d.tl) : 0ull);
+        if (off < d.dst_len) {
+            const uint32_t Ln = std::min<uint32_t>(len, d.dst_len - (uint32_t)off);
+            if (C.lane < Ln) {
+                d.val[off + C.lane] = d.src[(size_t)pos + C.lane];
+                d.idx[off + C.lane] = pos + C.lane + (uint32_t)d.idx_offset;
             }
         }
-        bef = wave_sum64(bef);
-        tot = wave_sum64(tot);
-        wbef = wave_sum64(wbef);
-        wtot = wave_sum64(wtot);
+    }
+    __syncthreads();  // L.cand is reused
+}
+
+// ---- finish(b): exchange, regime, emission, AIMD; regime B heap fill ----
+template <int STAGE>
+__device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &cr) {
+    const BucketDesc &d = C.A.bk[b];
+    Lds &L = C.L;
+    FillCtl *ctl = C.A.ctl;
+    const uint32_t par = b & 1u;
+    const uint32_t G = C.G, w = C.w, tid = C.tid, lane = C.lane, wave = C.wave;
+    const uint32_t L0 = C.range_lo(d.nb), nl = C.range_len(d.nb);
+    const bool lds_sums = nl <= LINES_B;
+    const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.idx) |
+                       reinterpret_cast<uintptr_t>(d.val)) & 15u) == 0;
+    auto get_sum = [&](uint32_t i) -> float { return lds_sums ? L.sum[par][i] : d.sums_g[L0 + i]; };
+    const float t = cr.t, inc = cr.inc;
+    const uint32_t tb = f2u(t);
+    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;
+    const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
+    BucketCtl *bc = &ctl->cc[C.A.epoch & 1u].bk[b];
+    uint64_t *cand = C.A.cand + (size_t)(b & 3u) * CAND_CAP;
+
+    // ---- count exchange: wave j gathers workgroups [64j, 64j+64) (one
+    //      granule pair per lane, all in flight), re-polling only stale ones ----
+    const uint32_t nsw = (G + 63) / 64;
+    if (wave < nsw) {
+        const uint32_t tg = C.tag(b);
+        const uint32_t v = wave * 64 + lane;
+        uint64_t g = 0, g2 = 0;
+        bool pend = v < G;
+        for (uint32_t spins = 0;; ++spins) {
+            if (pend) {
+                g = ld_sc1(&ctl->gran[b][v]);
+                g2 = ld_sc1(&ctl->gran2[b][v]);
+                pend = (uint32_t)(g >> 32) != tg || (uint32_t)(g2 >> 32) != tg;
+            }
+            if (!__any(pend)) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (spins > (1u << 22)) { atomicOr(C.A.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+        }
+        const uint32_t c = v < G ? (uint32_t)g : 0u, cw = v < G ? (uint32_t)g2 : 0u;
+        const uint32_t tot = wave_sum(c), wtot = wave_sum(cw);
+        const uint32_t bef = wave_sum(v < w ? c : 0u), wbef = wave_sum(v < w ? cw : 0u);
         if (lane == 0) {
-            s_dec[0] = (uint32_t)bef;
-            s_dec[1] = (uint32_t)tot;
-            s_dec[5] = (uint32_t)wtot;
-            s_dec[6] = (uint32_t)wbef;
+            L.xch[wave][0] = bef;
+            L.xch[wave][1] = tot;
+            L.xch[wave][2] = wbef;
+            L.xch[wave][3] = wtot;
         }
     }
     __syncthreads();
-    const uint32_t P = s_dec[0];
-    const uint32_t Qtot = s_dec[1];
-    const uint32_t Wtot = s_dec[5];
-    const uint32_t Wbef = s_dec[6];
-    if (STAGE == 2) return;
+    uint32_t P = 0, Qtot = 0, Wbef = 0, Wtot = 0;
+    for (uint32_t j = 0; j < nsw; ++j) {
+        P += L.xch[j][0];
+        Qtot += L.xch[j][1];
+        Wbef += L.xch[j][2];
+        Wtot += L.xch[j][3];
+    }
+    __syncthreads();
+    if (STAGE == 2) return Defer{};
 
-    STAMP(2);
-    // ---- 3. regime (identical in every workgroup) ----
-    const uint32_t lim = a.kb + (a.r ? 1u : 0u);
-    const uint32_t c0 = Qtot >= lim ? a.dst_len : 16u * Qtot;
-    bool tail_q = false, tail_cand = false;
+    // ---- regime (identical in every workgroup) ----
+    const uint32_t lim = kb + (r ? 1u : 0u);
+    const uint32_t c0 = Qtot >= lim ? d.dst_len : 16u * Qtot;
+    bool tail_cand = false;
     float tail_key = 0.f;
     uint32_t ct = 0;
-    if (c0 < a.dst_len && a.tl) {
-        const float *tp = a.src + (size_t)a.nb * 16;
+    if (c0 < d.dst_len && d.tl) {
+        const float *tp = d.src + (size_t)d.nb * 16;
         float s = 0.f;
-        for (uint32_t i = 0; i < a.tl; ++i) s += tp[i];
-        tail_q = s * 16.0f >= t * (float)a.tl;
-        if (tail_q) ct = std::min(a.dst_len - c0, a.tl);
-        else { tail_cand = true; tail_key = s * 16.0f / (float)a.tl; }
+        for (uint32_t i = 0; i < d.tl; ++i) s += tp[i];
+        if (s * 16.0f >= t * (float)d.tl) ct = std::min(d.dst_len - c0, d.tl);
+        else { tail_cand = true; tail_key = s * 16.0f / (float)d.tl; }
     }
     const uint32_t cnt = c0 + ct;
-    const bool regimeB = cnt < a.dst_len;
+    const bool regimeB = cnt < d.dst_len;
 
-    // ---- 3b. ordered emission of this range's qualifying lines ----
+    // ---- ordered emission of this range's qualifying lines ----
     // In-range rank of line i = j*FWG + tid via ballot masks (order j, wave, lane).
-    if (P < lim && Qw) {
+    if (P < lim && cr.qw) {
         const uint32_t nj = (nl + FWG - 1) / FWG;
-        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        if (nj <= MAX_J && Qw <= STAGE_LINES) {
+        if (nj <= MAX_J && cr.qw <= STAGE_B) {
             // every qualifying line is staged in LDS: one thread per staged line
             for (uint32_t j = 0; j < nj; ++j) {
                 const uint32_t i = j * FWG + tid;
                 const uint64_t bal = __ballot(i < nl && get_sum(i) >= t);
-                if (lane == 0) { s_mask[j * FNW + wave] = bal; s_wt[j * FNW + wave] = (uint32_t)__popcll(bal); }
+                if (lane == 0) { L.mask[j * FNW + wave] = bal; L.wt[j * FNW + wave] = (uint32_t)__popcll(bal); }
             }
             __syncthreads();
             if (tid == 0) {
                 uint32_t acc = 0;
-                for (uint32_t i = 0; i < nj * FNW; ++i) { const uint32_t x = s_wt[i]; s_wt[i] = acc; acc += x; }
+                for (uint32_t i = 0; i < nj * FNW; ++i) { const uint32_t x = L.wt[i]; L.wt[i] = acc; acc += x; }
             }
             __syncthreads();
-            for (uint32_t e = tid; e < Qw; e += FWG) {
-                const uint32_t i = s_stage_line[e];
+            for (uint32_t e = tid; e < cr.qw; e += FWG) {
+                const uint32_t i = L.stage_line[par][e];
                 const uint32_t grp = (i / FWG) * FNW + ((i % FWG) >> 6), ln = i & 63;
-                const uint64_t m = s_mask[grp];
-                const uint32_t g = P + s_wt[grp] + (uint32_t)__popcll(m & (ln ? (~0ull >> (64 - ln)) : 0ull));
+                const uint64_t m = L.mask[grp];
+                const uint32_t g = P + L.wt[grp] + (uint32_t)__popcll(m & (ln ? (~0ull >> (64 - ln)) : 0ull));
                 if (g < lim) {
                     const uint32_t pos = (L0 + i) * 16;
-                    const uint32_t len = g == a.kb ? a.r : 16u;
+                    const uint32_t len = g == kb ? r : 16u;
                     const uint32_t off = 16 * g;
-                    if (VEC && len == 16) {
-                        float4 *v4 = reinterpret_cast<float4 *>(a.val + off);
-                        uint4 *i4 = reinterpret_cast<uint4 *>(a.idx + off);
-                        const uint32_t bi = pos + (uint32_t)a.idx_offset;
+                    if (vec && len == 16) {
+                        float4 *v4 = reinterpret_cast<float4 *>(d.val + off);
+                        uint4 *i4 = reinterpret_cast<uint4 *>(d.idx + off);
+                        const uint32_t bi = pos + (uint32_t)d.idx_offset;
 #pragma unroll
                         for (uint32_t c = 0; c < 4; ++c) {
-                            v4[c] = s_stage[e * 4 + c];
+                            v4[c] = L.stage[par][e * 4 + c];
                             i4[c] = make_uint4(bi + 4 * c, bi + 4 * c + 1, bi + 4 * c + 2, bi + 4 * c + 3);
                         }
                     } else {
-                        const float *sv = reinterpret_cast<const float *>(&s_stage[e * 4]);
+                        const float *sv = reinterpret_cast<const float *>(&L.stage[par][e * 4]);
                         for (uint32_t c = 0; c < len; ++c) {
-                            a.val[off + c] = sv[c];
-                            a.idx[off + c] = pos + c + (uint32_t)a.idx_offset;
+                            d.val[off + c] = sv[c];
+                            d.idx[off + c] = pos + c + (uint32_t)d.idx_offset;
                         }
                     }
                 }
             }
+            __syncthreads();
         } else {
-            // staging overflowed (low threshold): re-read the lines from src
+            // staging overflowed (low threshold) or a long range: re-read src
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
             uint32_t base = P;
             for (uint32_t j0 = 0; j0 < nj && base < lim; j0 += MAX_J) {
                 const uint32_t jn = std::min(nj - j0, MAX_J);
@@ -396,90 +482,85 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                     const bool f = i < nl && get_sum(i) >= t;
                     flags |= (uint32_t)f << j;
                     const uint64_t bal = __ballot(f);
-                    if (lane == 0) s_wt[j * FNW + wave] = (uint32_t)__popcll(bal);
+                    if (lane == 0) L.wt[j * FNW + wave] = (uint32_t)__popcll(bal);
                 }
                 __syncthreads();
                 if (tid == 0) {
                     uint32_t acc = 0;
-                    for (uint32_t i = 0; i < jn * FNW; ++i) { const uint32_t x = s_wt[i]; s_wt[i] = acc; acc += x; }
-                    s_wt[MAX_J * FNW] = acc;
+                    for (uint32_t i = 0; i < jn * FNW; ++i) { const uint32_t x = L.wt[i]; L.wt[i] = acc; acc += x; }
+                    L.wt[MAX_J * FNW] = acc;
                 }
                 __syncthreads();
                 for (uint32_t j = 0; j < jn; ++j) {
                     const uint64_t bal = __ballot((flags >> j) & 1u);
                     if ((flags >> j) & 1u) {
-                        const uint32_t g = base + s_wt[j * FNW + wave] + (uint32_t)__popcll(bal & lt);
+                        const uint32_t g = base + L.wt[j * FNW + wave] + (uint32_t)__popcll(bal & lt);
                         if (g < lim) {
                             const uint32_t line = L0 + (j0 + j) * FWG + tid;
-                            emit_line<VEC>(a, line * 16, 16 * g, g == a.kb ? a.r : 16u);
+                            emit_line(d, vec, line * 16, 16 * g, g == kb ? r : 16u);
                         }
                     }
                 }
-                base += s_wt[MAX_J * FNW];
+                base += L.wt[MAX_J * FNW];
                 __syncthreads();
             }
         }
     }
 
-    STAMP(3);
-    // ---- 4. tail, AIMD, count (workgroup 0) ----
-    if (w == 0) {  // zero the next call's counters (this call never touches them)
-        uint32_t *z = reinterpret_cast<uint32_t *>(&ctl->cc[(a.epoch + 1) & 1u]);
-        for (uint32_t i = tid; i < sizeof(CallCtl) / 4; i += FWG) st_sc1(z + i, 0u);
-    }
+    // ---- tail, AIMD, count (workgroup 0) ----
     if (w == 0 && tid == 0) {
         if (ct) {
-            const size_t p0 = (size_t)a.nb * 16;
+            const size_t p0 = (size_t)d.nb * 16;
             for (uint32_t i = 0; i < ct; ++i) {
-                a.val[c0 + i] = a.src[p0 + i];
-                a.idx[c0 + i] = (uint32_t)(p0 + i) + (uint32_t)a.idx_offset;
+                d.val[c0 + i] = d.src[p0 + i];
+                d.idx[c0 + i] = (uint32_t)(p0 + i) + (uint32_t)d.idx_offset;
             }
         }
-        a.state->t = regimeB ? (float)((double)t * 0.99) : t + inc;
-        a.state->inc = inc;
-        a.state->init = 1;
-        *a.count_out = (uint32_t)std::min<uint64_t>(a.dst_len, a.n);
+        d.state->t = regimeB ? (float)((double)t * 0.99) : t + inc;
+        d.state->inc = inc;
+        d.state->init = 1;
+        *d.count_out = (uint32_t)std::min<uint64_t>(d.dst_len, (uint64_t)d.nb * 16 + d.tl);
     }
-    if (!regimeB) return;
+    if (!regimeB) return Defer{};
 
-    // ---- 5. heap fill = top candidates by (sum desc, position asc) ----
-    const uint32_t rem = a.dst_len - cnt;
-    const uint32_t nc = a.nb - Qtot;  // non-qualifying full lines
-    const uint32_t M = std::min((rem + 15u) / 16u, nc);
-    const uint32_t hi0 = tb - 1u;     // largest candidate key (keys u < tb)
-    uint32_t nbar = 0;
+    // ---- heap fill = top candidates by (sum desc, position asc) ----
+    const uint32_t rem = d.dst_len - cnt;
+    const uint32_t ncand = d.nb - Qtot;  // non-qualifying full lines
+    const uint32_t M = std::min((rem + 15u) / 16u, ncand);
+    const uint32_t hi0 = tb - 1u;        // largest candidate key (keys u < tb)
 
     // mode 1: collect keys >= blo; mode 2: ties at ustar taken in position order
     uint32_t mode = 1, blo = tb, ustar = 0, greater = 0;
-    if (M > 0 && Wtot >= M && Wtot + 1 <= SORT_CAP) {
+    const bool win_ok = M > 0 && Wtot >= M && Wtot + 1 <= CAND_CAP;
+    if (win_ok) {
         blo = wlo;  // the window holds the top M: no histogram needed
     } else if (M > 0) {
-        for (uint32_t i = tid; i < HBINS; i += FWG) s_hist[i] = 0;
+        for (uint32_t i = tid; i < HBINS; i += FWG) L.hist[i] = 0;
         __syncthreads();
         for (uint32_t i = tid; i < nl; i += FWG) {
             const uint32_t u = f2u(get_sum(i));
-            if (u < tb) atomicAdd(&s_hist[std::min((hi0 - u) >> L1_SHIFT, HBINS - 1)], 1u);
+            if (u < tb) atomicAdd(&L.hist[std::min((hi0 - u) >> L1_SHIFT, HBINS - 1)], 1u);
         }
         __syncthreads();
         for (uint32_t i = tid; i < HBINS; i += FWG)
-            if (s_hist[i]) atomicAdd(&cc->hist[0][i], s_hist[i]);
-        grid_sync(++nbar);
+            if (L.hist[i]) atomicAdd(&bc->hist[0][i], L.hist[i]);
+        C.grid_sync();
         uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
         bool ovf = true;
         for (;;) {
             // locate the bin holding rank `need` (1-based) counting down from hi
             const uint32_t need = M - above;
-            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&cc->hist[lvl][tid]) : 0u;
+            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&bc->hist[lvl][tid]) : 0u;
             uint32_t total;
-            const uint32_t before = blk_excl_scan<FNW>(cbin, sh, &total);
-            if (tid == 0) { s_dec[2] = 0xffffffffu; s_dec[3] = 0; s_dec[4] = 0; }
+            const uint32_t before = blk_excl_scan<FNW>(cbin, L.sh, &total);
+            if (tid == 0) { L.dec[2] = 0xffffffffu; L.dec[3] = 0; L.dec[4] = 0; }
             __syncthreads();
-            if (tid < HBINS && need > before && need <= before + cbin) { s_dec[2] = tid; s_dec[3] = before; s_dec[4] = cbin; }
+            if (tid < HBINS && need > before && need <= before + cbin) { L.dec[2] = tid; L.dec[3] = before; L.dec[4] = cbin; }
             __syncthreads();
-            const uint32_t bstar = s_dec[2], cum = s_dec[3], hb = s_dec[4];
+            const uint32_t bstar = L.dec[2], cum = L.dec[3], hb = L.dec[4];
             __syncthreads();
             if (bstar == 0xffffffffu) {  // histogram does not reach `need`: collect all
-                if (tid == 0) atomicOr(a.fail, (uint32_t)FAIL_LEVELS);
+                if (tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_LEVELS);
                 mode = 1; blo = 0;
                 break;
             }
@@ -487,7 +568,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                 above += cum;
                 const uint64_t width = (uint64_t)(HBINS - 1) << s;
                 if ((uint64_t)hi < width) {
-                    if (tid == 0) atomicOr(a.fail, (uint32_t)FAIL_LEVELS);
+                    if (tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_LEVELS);
                     mode = 1; blo = 0;
                     break;
                 }
@@ -500,7 +581,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                 const int64_t blo64 = (int64_t)hi - ((int64_t)(bstar + 1) << s) + 1;
                 const uint32_t bl = (uint32_t)std::max<int64_t>((int64_t)lo, blo64);
                 const uint32_t totc = above + cum + hb;
-                if (totc + 1 <= SORT_CAP) { mode = 1; blo = bl; break; }
+                if (totc + 1 <= CAND_CAP) { mode = 1; blo = bl; break; }
                 if (s == 0) { mode = 2; ustar = bhi; greater = above + cum; break; }
                 above += cum;
                 hi = bhi;
@@ -508,31 +589,29 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                 s = s >= 10 ? s - 10 : 0;
             }
             if (++lvl >= MAX_LEVELS) {
-                if (tid == 0) atomicOr(a.fail, (uint32_t)FAIL_LEVELS);
+                if (tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_LEVELS);
                 mode = 1; blo = lo;
                 break;
             }
-            for (uint32_t i = tid; i < HBINS; i += FWG) s_hist[i] = 0;
+            for (uint32_t i = tid; i < HBINS; i += FWG) L.hist[i] = 0;
             __syncthreads();
             for (uint32_t i = tid; i < nl; i += FWG) {
                 const uint32_t u = f2u(get_sum(i));
-                if (u < tb && u >= lo && u <= hi) atomicAdd(&s_hist[(hi - u) >> s], 1u);
+                if (u < tb && u >= lo && u <= hi) atomicAdd(&L.hist[(hi - u) >> s], 1u);
             }
             __syncthreads();
             for (uint32_t i = tid; i < HBINS; i += FWG)
-                if (s_hist[i]) atomicAdd(&cc->hist[lvl][i], s_hist[i]);
-            grid_sync(++nbar);
+                if (L.hist[i]) atomicAdd(&bc->hist[lvl][i], L.hist[i]);
+            C.grid_sync();
         }
     }
 
-    STAMP(4);
-    const uint32_t tailpos = a.nb * 16;
+    const uint32_t tailpos = d.nb * 16;
     const bool tail_in_greater = tail_cand && mode == 2 && tail_key > u2f(ustar);
     // collect (write-through): mode 1 -> keys in [blo, tb); mode 2 -> keys in (ustar, tb).
     // The window path knows every workgroup's slot range from the exchanged
     // window counts (no atomics); the rare histogram paths append with one
     // atomic per workgroup and step.
-    const bool win_path = mode == 1 && blo == wlo && M > 0 && Wtot >= M && Wtot + 1 <= SORT_CAP;
     if (M > 0) {
         const uint32_t kmin = mode == 1 ? blo : ustar + 1;
         uint32_t mine = 0, run = Wbef;
@@ -546,148 +625,211 @@ __global__ void __launch_bounds__(FWG, 8) tv16_fused(FusedArgs a) {
                 mine += mode == 2 && u == ustar;
             }
             uint32_t n_here;
-            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, sh, &n_here);
+            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, L.sh, &n_here);
             if (!n_here) continue;
             uint32_t base;
-            if (win_path) {
+            if (win_ok) {
                 base = run;
                 run += n_here;
             } else {
-                if (tid == 0) s_dec[7] = atomicAdd(&cc->cand_n, n_here);
+                if (tid == 0) L.dec[7] = atomicAdd(&bc->cand_n, n_here);
                 __syncthreads();
-                base = s_dec[7];
+                base = L.dec[7];
                 __syncthreads();
             }
-            if (p && base + ex < SORT_CAP)
-                st_sc1(&a.cand[base + ex], ((uint64_t)(~(u | 0x80000000u)) << 32) | (uint64_t)((L0 + i) * 16));
+            if (p && base + ex < CAND_CAP)
+                st_sc1(&cand[base + ex], ((uint64_t)(~(u | 0x80000000u)) << 32) | (uint64_t)((L0 + i) * 16));
         }
         if (mode == 2) {
-            const uint32_t my_ties = (uint32_t)blk_sum64<FNW>(mine, sh64);
-            if (tid == 0) st_sc1(&ctl->wg_ties[w], my_ties);
+            const uint32_t my_ties = (uint32_t)blk_sum64<FNW>(mine, L.sh64);
+            if (tid == 0) st_sc1(&ctl->wg_ties[b & 3u][w], my_ties);
         }
     }
-    STAMP(5);
-    grid_sync(++nbar);  // every append / tie count is visible
-    STAMP(6);
-    if (mode == 2) {
+    if (mode == 1) {
+        // The common case: publish "candidates written" and rank the set
+        // after the next bucket's scan (rank_deferred), when every workgroup's
+        // candidates are long in place -- no grid barrier on the critical path.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) st_sc1(&ctl->cdone[b][w], (uint64_t)C.tag(b) << 32);
+        Defer D;
+        D.active = 1;
+        D.b = b;
+        D.cnt = cnt;
+        D.nc = win_ok ? Wtot : 0xffffffffu;
+        D.tail_cand = tail_cand ? 1u : 0u;
+        D.tail_key = tail_key;
+        return D;
+    }
+    C.grid_sync();  // every append / tie count is visible
+    {  // mode 2: lines tied at ustar, in position order after the greater keys
         uint64_t pb = 0, pt = 0;
         for (uint32_t i = tid; i < G; i += FWG) {
-            const uint32_t x = ld_acq_relaxed(&ctl->wg_ties[i]);
+            const uint32_t x = ld_acq_relaxed(&ctl->wg_ties[b & 3u][i]);
             pt += x;
             if (i < w) pb += x;
         }
-        uint32_t rank = (uint32_t)blk_sum64<FNW>(pb, sh64);
-        const uint32_t all_ties = (uint32_t)blk_sum64<FNW>(pt, sh64);
-        const uint32_t base = cnt + 16u * greater + (tail_in_greater ? a.tl : 0u);
+        uint32_t rank = (uint32_t)blk_sum64<FNW>(pb, L.sh64);
+        const uint32_t all_ties = (uint32_t)blk_sum64<FNW>(pt, L.sh64);
+        const uint32_t base = cnt + 16u * greater + (tail_in_greater ? d.tl : 0u);
         for (uint32_t i0 = 0; i0 < nl; i0 += FWG) {
             const uint32_t i = i0 + tid;
             const bool p = i < nl && f2u(get_sum(i)) == ustar;
             uint32_t n_here;
-            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, sh, &n_here);
+            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, L.sh, &n_here);
             if (p) {
                 const uint64_t off = (uint64_t)base + 16ull * (rank + ex);
-                if (off < a.dst_len)
-                    emit_line<VEC>(a, (L0 + i) * 16, (uint32_t)off, std::min<uint32_t>(16u, a.dst_len - (uint32_t)off));
+                if (off < d.dst_len)
+                    emit_line(d, vec, (L0 + i) * 16, (uint32_t)off, std::min<uint32_t>(16u, d.dst_len - (uint32_t)off));
             }
             rank += n_here;
         }
         if (w == 0 && tid == 0 && tail_cand && tail_key == u2f(ustar)) {
             const uint64_t off = (uint64_t)base + 16ull * all_ties;
-            if (off < a.dst_len)
-                emit_line<false>(a, tailpos, (uint32_t)off, std::min<uint32_t>(a.tl, a.dst_len - (uint32_t)off));
+            if (off < d.dst_len)
+                emit_line(d, false, tailpos, (uint32_t)off, std::min<uint32_t>(d.tl, d.dst_len - (uint32_t)off));
         }
-        __syncthreads();  // line sums in s_buf are dead from here on
     }
+    uint32_t nc_all = ld_acq_relaxed(&bc->cand_n);
+    if (nc_all > CAND_CAP) {
+        if (w == 0 && tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_CAND_OVERFLOW);
+        nc_all = CAND_CAP;
+    }
+    rank_emit(C, d, cand, cnt, nc_all, tail_in_greater && nc_all < CAND_CAP, tail_key);
+    return Defer{};
+}
 
-    // ---- distributed rank-and-emit of the collected set ----
-    // Output order is (sum desc, position asc) = ascending composite key
-    // (~ord(sum) << 32 | pos); an entry's rank is the number of smaller keys,
-    // counted by one wave per entry over the LDS copy of the set.
-    uint32_t nc_all = win_path ? Wtot : ld_acq_relaxed(&cc->cand_n);
-    if (nc_all > SORT_CAP) {
-        if (w == 0 && tid == 0) atomicOr(a.fail, (uint32_t)FAIL_CAND_OVERFLOW);
-        nc_all = SORT_CAP;
-    }
-    const bool add_tail = tail_cand && (mode == 1 || tail_in_greater) && nc_all < SORT_CAP;
-    const uint32_t total = nc_all + (add_tail ? 1u : 0u);
-    const uint32_t first_e = w * FNW;  // entries handled here: e = w*FNW + wave + k*G*FNW
-    if (first_e >= total) return;
-    const uint64_t tail_comp = ((uint64_t)(~ford(tail_key)) << 32) | (uint64_t)tailpos;
-    __syncthreads();
-    for (uint32_t i = tid; i < total; i += FWG) s_buf[i] = i < nc_all ? ld_sc1(&a.cand[i]) : tail_comp;
-    __syncthreads();
-    for (uint32_t e = first_e + wave; e < total; e += G * FNW) {
-        const uint64_t key = s_buf[e];
-        uint32_t less = 0;
-        for (uint32_t j = lane; j < total; j += 64) less += s_buf[j] < key;
-        const uint32_t rank = wave_sum(less);
-        const bool is_tail = add_tail && key == tail_comp;
-        const bool tail_before = add_tail && tail_comp < key;
-        const uint32_t pos = (uint32_t)key;
-        const uint32_t len = is_tail ? a.tl : 16u;
-        const uint64_t off = (uint64_t)cnt + 16ull * rank - (tail_before ? (uint64_t)(16u - a.tl) : 0ull);
-        if (off < a.dst_len) {
-            const uint32_t L = std::min<uint32_t>(len, a.dst_len - (uint32_t)off);
-            if (lane < L) {
-                a.val[off + lane] = a.src[(size_t)pos + lane];
-                a.idx[off + lane] = pos + lane + (uint32_t)a.idx_offset;
-            }
+// Deferred rank-and-emit of a mode-1 candidate set (bucket D.b), run one
+// bucket later.  Workgroups with no entries to rank return at once when the
+// set size is known (window path); the others wait for every workgroup's
+// "candidates written" tag (normally already set) and rank.
+__device__ __forceinline__ void rank_deferred(Ctx &C, const Defer &D) {
+    if (!D.active) return;
+    const BucketDesc &d = C.A.bk[D.b];
+    const uint32_t first_e = C.w * FNW;
+    if (D.nc != 0xffffffffu && first_e >= D.nc + (D.tail_cand && D.nc < CAND_CAP ? 1u : 0u)) return;
+    Lds &L = C.L;
+    const uint32_t nsw = (C.G + 63) / 64;
+    if (C.wave < nsw) {
+        const uint32_t tg = C.tag(D.b);
+        const uint32_t v = C.wave * 64 + C.lane;
+        bool pend = v < C.G;
+        for (uint32_t spins = 0;; ++spins) {
+            if (pend) pend = (uint32_t)(ld_sc1(&C.A.ctl->cdone[D.b][v]) >> 32) != tg;
+            if (!__any(pend)) break;
+            __builtin_amdgcn_s_sleep(2);
+            if (spins > (1u << 22)) { atomicOr(C.A.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
         }
     }
-    STAMP(7);
-#undef STAMP
+    __syncthreads();
+    uint32_t nc_all = D.nc;
+    if (nc_all == 0xffffffffu) nc_all = ld_acq_relaxed(&C.A.ctl->cc[C.A.epoch & 1u].bk[D.b].cand_n);
+    if (nc_all > CAND_CAP) {
+        if (C.tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_CAND_OVERFLOW);
+        nc_all = CAND_CAP;
+    }
+    (void)L;
+    rank_emit(C, d, C.A.cand + (size_t)(D.b & 3u) * CAND_CAP, D.cnt, nc_all, D.tail_cand && nc_all < CAND_CAP,
+              D.tail_key);
+}
+
+// STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = return
+// after the streaming passes; 2 = skip everything after the count exchanges;
+// 3 = plain streaming read (calibration); 4 = full codec + per-workgroup
+// s_memrealtime stamps: stamps[w*16 + 15] at start, [w*16 + 2b] after scan(b),
+// [w*16 + 2b + 1] after finish(b) and the deferred rank of b-1 (b < 7),
+// [w*16 + 14] = XCC id.
+template <int STAGE>
+__global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
+    __shared__ Lds L;
+    Ctx C{A, L, gridDim.x, blockIdx.x, threadIdx.x, __lane_id(), (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), 0};
+    auto stamp = [&](uint32_t k) {
+        if (STAGE == 4 && C.tid == 0 && k < 16)
+            A.stamps[C.w * 16 + k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    };
+    stamp(15);
+    if (STAGE == 4 && C.tid == 0)
+        A.stamps[C.w * 16 + 14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+
+    {  // zero the next call's per-call counters (this call never touches them)
+        uint32_t *z = reinterpret_cast<uint32_t *>(&A.ctl->cc[(A.epoch + 1) & 1u]);
+        constexpr uint32_t words = sizeof(CallCtl) / 4;
+        const uint32_t per = (words + C.G - 1) / C.G;
+        const uint32_t z0 = C.w * per, z1 = std::min(words, z0 + per);
+        for (uint32_t i = z0 + C.tid; i < z1; i += FWG) st_sc1(z + i, 0u);
+    }
+    // software pipeline: scan(b) | finish(b-1) | deferred rank of b-2
+    Carry prev{}, cur{};  // scan results of bucket b-1 and b (no indexed locals: no scratch)
+    Defer pend{};         // regime-B set of bucket b-2 awaiting its rank-and-emit
+    for (uint32_t b = 0; b <= A.nbk + 1; ++b) {
+        if (b < A.nbk) {
+            // ranges beyond LINES_B keep their line sums in global scratch
+            if (C.range_len(A.bk[b].nb) <= LINES_B) cur = scan_bucket<STAGE, true>(C, b);
+            else cur = scan_bucket<STAGE, false>(C, b);
+            if (b < 7) stamp(2 * b);
+        }
+        if (STAGE == 1 || STAGE == 3) continue;
+        Defer dn{};
+        if (b > 0 && b <= A.nbk) dn = finish_bucket<STAGE>(C, b - 1, prev);
+        rank_deferred(C, pend);
+        if (b > 0 && b - 1 < 7) stamp(2 * (b - 1) + 1);
+        pend = dn;
+        prev = cur;
+    }
 }
 
 }  // namespace
 
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
-    const uint32_t nb = (uint32_t)(a.n / 16);
-    const uint32_t tl = (uint32_t)(a.n % 16);
-    if (a.first) {
-        const uint32_t nblk = (uint32_t)((a.n + 15) / 16);
-        tv16_seq_sums<<<(nblk + STG_WG - 1) / STG_WG, STG_WG, 0, s>>>(a.src, a.n, ws.sums, nblk);
-        const uint32_t bk = std::min<uint32_t>(a.k / 16, nblk - 1);
-        hipError_t e = launch_radix_select(ws.sums, nblk, 0xffffffffu, 0, nullptr, bk, ws, a.num_cu, s);
-        if (e != hipSuccess) return e;
-        tv16_init_state<<<1, 1, 0, s>>>(a.state, ws.rsel);
+    if (!a.nb) return hipSuccess;
+    if (a.nb > MAX_BATCH || !a.epoch || a.epoch >= (1u << 24)) return hipErrorInvalidValue;
+    BatchArgs A{};
+    uint32_t max_nb = 1;
+    for (uint32_t i = 0; i < a.nb; ++i) {
+        const Tv16Bucket &b = a.b[i];
+        if (b.first) {  // first threshold from sequential line sums (thresholdv16.cpp:36-54)
+            const uint32_t nblk = (uint32_t)((b.n + 15) / 16);
+            tv16_seq_sums<<<(nblk + STG_WG - 1) / STG_WG, STG_WG, 0, s>>>(b.src, b.n, b.sums, nblk);
+            const uint32_t bk = std::min<uint32_t>(b.k / 16, nblk - 1);
+            hipError_t e = launch_radix_select(b.sums, nblk, 0xffffffffu, 0, nullptr, bk, ws, a.num_cu, s);
+            if (e != hipSuccess) return e;
+            tv16_init_state<<<1, 1, 0, s>>>(b.state, ws.rsel);
+        }
+        BucketDesc &d = A.bk[i];
+        d.src = b.src;
+        d.idx = b.idx;
+        d.val = b.val;
+        d.count_out = b.count_out;
+        d.state = b.state;
+        d.sums_g = b.sums;
+        d.nb = (uint32_t)(b.n / 16);
+        d.tl = (uint32_t)(b.n % 16);
+        d.dst_len = b.dst_len;
+        d.idx_offset = b.idx_offset;
+        max_nb = std::max(max_nb, d.nb);
     }
+    A.nbk = a.nb;
+    A.epoch = a.epoch;
+    A.ctl = ws.ctl;
+    A.cand = ws.cand;
+    A.fail = ws.fail;
+    A.stamps = a.b[a.nb - 1].count_out + 1;  // STAGE 4: words after the last bucket's count
     // wg_per_cu 1024-thread workgroups per CU (2: 32 waves, full occupancy for
-    // one call; 1: half, so two calls from two streams share the CUs), all
-    // co-resident for the in-launch exchanges, at least 1024 lines each
+    // one stream; 1: two launches from two streams share the CUs), all
+    // co-resident for the in-launch exchanges, >= 1024 lines of the largest
+    // bucket each
     const uint32_t G = std::max<uint32_t>(
-        1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, (nb + 1023) / 1024), MAX_FILL_WG));
-    const uint32_t per = (nb + G - 1) / G;
-    FusedArgs f;
-    f.src = a.src;
-    f.n = a.n;
-    f.nb = nb;
-    f.tl = tl;
-    f.dst_len = a.dst_len;
-    f.kb = a.dst_len / 16;
-    f.r = a.dst_len % 16;
-    f.epoch = a.epoch;
-    f.idx_offset = a.idx_offset;
-    f.idx = a.idx;
-    f.val = a.val;
-    f.count_out = a.count_out;
-    f.state = a.state;
-    f.sums_g = ws.sums;
-    f.ctl = ws.ctl;
-    f.cand = ws.cand;
-    f.fail = ws.fail;
-    const bool vec = ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(a.idx) |
-                       reinterpret_cast<uintptr_t>(a.val)) & 15u) == 0;
-    const bool lds = per <= LDS_LINES;
-    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+        1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, (max_nb + 1023) / 1024),
+                              MAX_FILL_WG));
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
-    if (dbg_stage == 1) tv16_fused<true, true, 1><<<G, FWG, 0, s>>>(f);
-    else if (dbg_stage == 2) tv16_fused<true, true, 2><<<G, FWG, 0, s>>>(f);
-    else if (dbg_stage == 3) tv16_fused<true, true, 3><<<G, FWG, 0, s>>>(f);
-    else if (dbg_stage == 4) tv16_fused<true, true, 4><<<G, FWG, 0, s>>>(f);
-    else if (vec && lds) tv16_fused<true, true><<<G, FWG, 0, s>>>(f);
-    else if (vec) tv16_fused<true, false><<<G, FWG, 0, s>>>(f);
-    else if (lds) tv16_fused<false, true><<<G, FWG, 0, s>>>(f);
-    else tv16_fused<false, false><<<G, FWG, 0, s>>>(f);
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    switch (dbg_stage) {
+        case 1: tv16_batch<1><<<G, FWG, 0, s>>>(A); break;
+        case 2: tv16_batch<2><<<G, FWG, 0, s>>>(A); break;
+        case 3: tv16_batch<3><<<G, FWG, 0, s>>>(A); break;
+        case 4: tv16_batch<4><<<G, FWG, 0, s>>>(A); break;
+        default: tv16_batch<0><<<G, FWG, 0, s>>>(A); break;
+    }
     if (a.ev) {
         (void)hipEventRecord(a.ev[1], s);
         (void)hipEventRecord(a.ev[2], s);

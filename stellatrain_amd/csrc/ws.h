@@ -12,7 +12,8 @@ constexpr uint32_t TV16_TILE_BLOCKS = 512;   // 16-float lines per scan tile (32
 constexpr uint32_t TV16_UNROLL = TV16_TILE_BLOCKS / (STG_WG / 4);  // 8 float4 per lane
 constexpr uint32_t HBINS = 1024;             // regime-B histogram bins per level
 constexpr uint32_t MAX_LEVELS = 6;           // regime-B radix-descent levels
-constexpr uint32_t SORT_CAP = 6144;          // regime-B candidates ranked in LDS (48 KiB)
+constexpr uint32_t CAND_CAP = 4096;          // regime-B candidates ranked in LDS per bucket
+constexpr uint32_t SORT_CAP = 4 * CAND_CAP;  // global candidate buffers: one per bucket % 4
 constexpr uint32_t MAX_FILL_WG = 1024;       // upper bound on fill-kernel workgroups
 
 constexpr uint32_t TV_TILE = 8192;           // threshold-v elements per tile (32 KiB)
@@ -20,28 +21,40 @@ constexpr uint32_t TV_STAGE = 512;           // staged qualifiers per threshold-
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 
-// thresholdv16 in-launch control block.
-// Per-call counters come in two copies selected by the call epoch's parity;
-// workgroup 0 zeroes the other copy for the next call (the next call on this
-// workspace is stream-ordered after this kernel).
-struct CallCtl {
-    uint32_t arrive;    // count-exchange arrivals
-    uint32_t bar;       // grid-barrier arrivals (round r completes at r * G)
+// thresholdv16 in-launch control block (one launch = a batch of <= MAX_BATCH
+// buckets).  Per-call counters come in two copies selected by the call
+// epoch's parity; every launch zeroes the other copy for the next call (the
+// next call on this workspace is stream-ordered after this launch).  Words
+// handed between workgroups carry a 32-bit tag {epoch:24 | bucket:8}.  The
+// count granules and "candidates written" tags are per bucket (a fast
+// workgroup may publish bucket b+2 while a slow one still gathers bucket b).
+// Regime-B candidates of bucket b are written in finish(b) (after scan(b+1))
+// and read in the deferred rank after scan(b+2); a workgroup can be writing
+// bucket b's set while a slow one still ranks b-1 or b-2 but never b-3, so the
+// candidate buffers and tie counts rotate over bucket % 4.
+constexpr uint32_t MAX_BATCH = 16;
+struct BucketCtl {
     uint32_t cand_n;    // regime-B candidates appended (histogram paths only)
-    uint32_t pad;
+    uint32_t pad[3];
     uint32_t hist[MAX_LEVELS][HBINS];
+};
+struct CallCtl {
+    uint32_t bar;       // grid-barrier arrivals (round r completes at r * G)
+    uint32_t pad[3];
+    BucketCtl bk[MAX_BATCH];
 };
 // One 128-byte line per workgroup, written by a barrier's last arriver and
 // polled only by its owner (no line is polled by more than one workgroup).
 struct alignas(128) WgSlot {
-    uint64_t go;        // {epoch:32 | barrier round:32}
+    uint64_t go;        // {epoch tag:32 | barrier round:32}
     uint64_t pad[15];
 };
 struct FillCtl {
-    CallCtl cc[2];
-    uint32_t wg_ties[MAX_FILL_WG];  // regime-B ties per workgroup (written before read)
-    uint64_t gran[MAX_FILL_WG];     // {epoch:32 | count:32}, never zeroed
-    uint64_t gran2[MAX_FILL_WG];    // {epoch:32 | window count:32}
+    CallCtl cc[2];                     // [epoch parity]
+    uint32_t wg_ties[4][MAX_FILL_WG];  // [bucket % 4] regime-B ties per workgroup
+    uint64_t gran[MAX_BATCH][MAX_FILL_WG];   // {tag:32 | count:32}, never zeroed
+    uint64_t gran2[MAX_BATCH][MAX_FILL_WG];  // {tag:32 | window count:32}
+    uint64_t cdone[MAX_BATCH][MAX_FILL_WG];  // {tag:32 | 0}: regime-B candidates written
     WgSlot slot[MAX_FILL_WG];
 };
 
@@ -66,7 +79,7 @@ struct DevWS {
     CallParams *cp;
     RSel *rsel;
     uint32_t *fail;      // sticky failure bits
-    uint64_t *cand;      // regime-B candidates (key << 32 | pos), SORT_CAP entries
+    uint64_t *cand;      // regime-B candidates (key << 32 | pos), CAND_CAP per bucket % 4
     uint32_t *misc;      // small scratch (counts)
     float *sums;         // thresholdv16: one sum per 16-float line
     uint32_t *tile_cnt;  // per-tile qualifier counts
@@ -76,7 +89,7 @@ struct DevWS {
 };
 
 // ---- launchers (implemented in the .hip files) ----
-struct Tv16Launch {
+struct Tv16Bucket {
     const float *src;
     size_t n;
     uint32_t k;
@@ -86,10 +99,15 @@ struct Tv16Launch {
     int32_t idx_offset;
     uint32_t *count_out;
     KeyState *state;
-    bool first;
+    bool first;        // no AIMD state yet: compute the first threshold
+    float *sums;       // per-bucket scratch (first threshold; ranges beyond LDS)
+};
+struct Tv16Launch {
+    const Tv16Bucket *b;
+    uint32_t nb;       // buckets in this launch (<= MAX_BATCH)
     int num_cu;
-    hipEvent_t *ev;  // optional [before, mid, after] the codec launch(es)
-    uint32_t epoch;  // per-workspace call counter, never 0 (granule tags)
+    hipEvent_t *ev;    // optional [before, mid, after] the codec launch(es)
+    uint32_t epoch;    // per-workspace call counter, 1..2^24-1 (hand-off tags)
     uint32_t wg_per_cu;  // fused-kernel workgroups per CU (1 or 2)
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);

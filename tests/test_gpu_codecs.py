@@ -205,3 +205,100 @@ def test_host_path_matches_device(gpu, oracle):
         val = np.zeros(k, np.float32)
         assert comp.compress("h", src, k, idx, val, 5) == co
         assert_same_pairs(idx, val, io, vo, co)
+
+
+# Batched launches: several buckets (distinct keys, mixed sizes incl. buckets
+# with fewer lines than workgroups, ragged tails, idx offsets) per persistent
+# launch, and a repeated key that must split the batch (its second call sees
+# the threshold the first call wrote).
+BATCH = [
+    ("b0@weight", 1000003, 10000, D1, 0),
+    ("b1@weight", 65536, 655, D2, 1 << 20),
+    ("b2@bias", 1000, 7, D1, 0),
+    ("b0@weight", 1000003, 10000, D1, 0),
+    ("b3@weight", 4096 + 7, 40, D1, 5),
+    ("b4@weight", 262144, 2621, D1, 0),
+    ("b5@weight", 33, 3, D1, 0),
+]
+
+
+@pytest.mark.parametrize("layout", ["mixed", "sixteen"])
+def test_thresholdv16_batch(gpu, oracle, layout):
+    import torch
+    from stellatrain_amd import ThresholdvCompressor16
+    if layout == "mixed":
+        spec = BATCH
+    else:  # a full batch of 16 distinct keys, then one more (17 -> two launches)
+        spec = [(f"s{i}@w", 131072 + 16 * i + (i % 3), 1311 + i, D1 if i % 2 else D2, 0) for i in range(17)]
+    comp = ThresholdvCompressor16()
+    ho = oracle.tv16_new()
+    for it in range(7):
+        items, ref = [], []
+        for j, (key, n, k, dist, off) in enumerate(spec):
+            src = synth(n, seed_for(40 + j, it), dist)
+            t_before = oracle.tv16_state(ho, key)
+            co, io, vo = oracle.tv16_compress(ho, key, src, k, idx_offset=off)
+            ref.append((src, co, io, vo, t_before, oracle.tv16_state(ho, key)))
+            items.append((key, torch.from_numpy(src).to(gpu), k, torch.zeros(k, dtype=torch.int32, device=gpu),
+                          torch.zeros(k, dtype=torch.float32, device=gpu), off))
+        counts = comp.compress_batch_async(items).cpu().numpy()
+        torch.cuda.synchronize()
+        for j, ((key, _, k, idx, val, off), (src, co, io, vo, t_before, _)) in enumerate(zip(items, ref)):
+            assert counts[j] == co, (it, j)
+            ig, vg = idx.cpu().numpy().view(np.uint32), val.cpu().numpy()
+            assert_same_pairs(ig, vg, io, vo, co)
+            head = _regime_split(oracle, src, k, t_before[0], co) if t_before is not None else 0
+            assert_same_stream(ig, vg, io, vo, head)
+        # final state of every key equals the oracle's after its last call
+        last = {}
+        for (key, *_), r in zip(spec, ref):
+            last[key] = r[5]
+        for key, so in last.items():
+            sg = comp.state(key)
+            assert bits(np.array(so, np.float32)).tolist() == bits(np.array(sg, np.float32)).tolist(), key
+    comp.check_device()
+    oracle.tv16_free(ho)
+
+
+def test_thresholdv16_batch_64mib(gpu, oracle):
+    """The bench workload: 8 x 64 MiB buckets per launch, k = 1%, against the
+    oracle for two keys of the batch over an AIMD sequence (both regimes)."""
+    import torch
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel
+    from stellatrain_amd.synth import seed_for as sf
+    n = 16 << 20
+    k = merge_numel(n, 0.99)
+    comp = ThresholdvCompressor16()
+    ho = oracle.tv16_new()
+    keys = [f"{i}@weight" for i in range(8)]
+    outs = [(torch.zeros(k, dtype=torch.int32, device=gpu), torch.zeros(k, dtype=torch.float32, device=gpu))
+            for _ in keys]
+    regimes = set()
+    for it in range(6):
+        srcs = [synth(n, sf(i, it)) if i in (0, 5) else None for i in range(8)]
+        dev = []
+        for i in range(8):
+            t = torch.empty(n, dtype=torch.float32, device=gpu)
+            if srcs[i] is not None:
+                t.copy_(torch.from_numpy(srcs[i]))
+            else:
+                from stellatrain_amd._capi import lib
+                import ctypes as C
+                lib().stg_synth_fill_device(C.c_void_p(t.data_ptr()), n, sf(i, it), 0, 0,
+                                            C.c_void_p(torch.cuda.current_stream().cuda_stream))
+            dev.append(t)
+        counts = comp.compress_batch_async(
+            [(keys[i], dev[i], k, outs[i][0], outs[i][1]) for i in range(8)]).cpu().numpy()
+        assert (counts == k).all()
+        for i in (0, 5):
+            t_before = oracle.tv16_state(ho, keys[i])
+            co, io, vo = oracle.tv16_compress(ho, keys[i], srcs[i], k)
+            ig, vg = outs[i][0].cpu().numpy().view(np.uint32), outs[i][1].cpu().numpy()
+            assert_same_pairs(ig, vg, io, vo, co)
+            so = oracle.tv16_state(ho, keys[i])
+            assert bits(np.array(so, np.float32)).tolist() == bits(np.array(comp.state(keys[i]), np.float32)).tolist()
+            if t_before is not None:
+                regimes.add("B" if so[0] < t_before[0] else "A")
+    comp.check_device()
+    oracle.tv16_free(ho)
+    assert regimes  # at least one steady-state call compared

@@ -28,26 +28,26 @@ for s in "$@"; do
         tests_all) step tests_all 900 python -m pytest tests -q -m gpu ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
         bench) step bench 400 python bench.py ;;
-        bench_short) step bench_short 300 python bench.py --steps 100 --warmup 16 --cpu-seconds 5 ;;
+        bench_short) step bench_short 300 python bench.py --steps 40 --warmup 8 --cpu-seconds 5 ;;
         breakdown) step breakdown 300 python tools/breakdown.py ;;
         breakdown_d3) step breakdown_d3 300 python tools/breakdown.py --dist 2 --param 9000 ;;
         prof) step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
-                -- python3 bench.py --steps 200 --warmup 32 --no-cpu-baseline ;;
+                -- python3 bench.py --steps 50 --warmup 8 --no-cpu-baseline ;;
         pmc_fetch) step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
-                -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline ;;
+                -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 16 --warmup 4 --profile-steps 4 --no-cpu-baseline ;;
         pmc_write) step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
-                -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 64 --warmup 16 --no-cpu-baseline ;;
+                -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 16 --warmup 4 --profile-steps 4 --no-cpu-baseline ;;
         prof_s1|prof_s2|prof_s3)
             export STG_DEBUG_TV16_STAGE=${s#prof_s}
             step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$s" -o run \
-                -- python3 bench.py --steps 200 --warmup 32 --no-cpu-baseline
+                -- python3 bench.py --steps 50 --warmup 8 --no-cpu-baseline
             unset STG_DEBUG_TV16_STAGE ;;
         ubench) step ubench 300 python tools/ubench_read.py ;;
         sweep)
-            for W in 1 2; do for S in 1 2 4; do
+            for W in 1 2; do for S in 1 2; do for K in 8 16; do
                 export STG_TV16_WGPERCU=$W
-                step sweep_w${W}_s${S} 200 python bench.py --steps 400 --warmup 32 --no-cpu-baseline --streams $S
-            done; done
+                step sweep_w${W}_s${S}_k${K} 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline --streams $S --keys $K
+            done; done; done
             unset STG_TV16_WGPERCU ;;
         stamps) export STG_DEBUG_TV16_STAGE=4; step stamps 300 python tools/stamps.py; unset STG_DEBUG_TV16_STAGE ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
