@@ -79,6 +79,14 @@ public:
             throw std::runtime_error(stg_last_error());
     }
 
+    /* Batched device-resident form: the engine's per-iteration set of MERGE
+     * compress tasks (compress.cpp:141 once per bucket) issued as one call;
+     * same results as compress_device on each bucket in order. */
+    void compress_batch_device(const stg_bucket_t *buckets, size_t n, void *stream) {
+        if (stg_codec_compress_batch_device(h_, buckets, n, stream) != STG_OK)
+            throw std::runtime_error(stg_last_error());
+    }
+
     stg_codec_t handle() { return h_; }
 };
 

@@ -44,8 +44,10 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 constexpr uint32_t FWG = 1024;     // workgroup: 16 waves
 constexpr uint32_t FNW = FWG / 64;
 constexpr uint32_t L1_SHIFT = 14;  // level-1 bin width in ulps below t (~0.2% of t)
-constexpr uint32_t LINES_B = 3072; // line sums kept in LDS per workgroup and bucket parity
-constexpr uint32_t STAGE_B = 128;  // qualifying lines staged in LDS per workgroup and parity
+constexpr uint32_t LA = 2;         // pipeline lookahead: finish(b) runs after scan(b + LA)
+constexpr uint32_t NBUF = LA + 1;  // LDS buffer sets (line sums, staged lines) in flight
+constexpr uint32_t LINES_B = 2048; // line sums kept in LDS per workgroup and buffer set
+constexpr uint32_t STAGE_B = 88;   // qualifying lines staged in LDS per workgroup and buffer set
 constexpr uint32_t SCAN_U = 8;     // float4 per lane per load batch
 constexpr uint32_t MAX_J = LINES_B / FWG;
 constexpr uint32_t WIN = 1u << 17; // regime-B window below t, in ulps (~1.6% of t)
@@ -85,7 +87,7 @@ __global__ void tv16_init_state(KeyState *st, const RSel *rs) {
 // ---------------------------------------------------------------------------
 // batched persistent kernel
 // ---------------------------------------------------------------------------
-struct BucketDesc {  // 64 bytes
+struct BucketDesc {  // 80 bytes
     const float *src;
     uint32_t *idx;
     float *val;
@@ -94,6 +96,8 @@ struct BucketDesc {  // 64 bytes
     float *sums_g;  // line sums of ranges beyond LINES_B
     uint32_t nb, tl, dst_len;
     int32_t idx_offset;
+    uint32_t per, rem;  // line ranges: workgroup w owns per + (w < rem) lines
+    uint32_t pad[2];
 };
 
 struct BatchArgs {
@@ -108,10 +112,13 @@ struct BatchArgs {
 
 // LDS of one workgroup (< 80 KiB: two workgroups per CU).
 struct Lds {
-    float sum[2][LINES_B];          // line sums, by bucket parity
-    float4 stage[2][STAGE_B * 4];   // staged qualifying lines (64 B each)
-    uint32_t stage_line[2][STAGE_B];
-    uint64_t cand[CAND_CAP];        // regime-B candidates (rank phase)
+    float sum[NBUF][LINES_B];       // line sums, by buffer set (bucket % NBUF)
+    float4 stage[NBUF][STAGE_B * 4];  // staged qualifying lines (64 B each)
+    uint32_t stage_line[NBUF][STAGE_B];
+    union {
+        uint64_t cand[CAND_CAP];    // regime-B candidates (rank phase)
+        uint4 pf[MAX_FILL_WG];      // previous bucket's granules (scan -> finish)
+    };
     uint64_t mask[MAX_J * FNW];
     uint32_t hist[HBINS];
     uint32_t wt[MAX_J * FNW + 1];
@@ -119,8 +126,9 @@ struct Lds {
     uint64_t sh64[FNW];
     uint32_t dec[8];
     uint32_t xch[FNW][4];           // count exchange partials per polling wave
-    uint32_t nst[2];
-    uint32_t cnt[2][2 * FNW];       // per-wave counts of a scan
+    uint32_t nst[NBUF];
+    uint32_t stamp[32];             // STAGE 4: timestamps, flushed at kernel end
+    uint32_t cnt[2 * FNW];          // per-wave counts of a scan
 };
 
 // Per-bucket values a workgroup carries from scan(b) to finish(b).
@@ -129,7 +137,18 @@ struct Carry {
     uint32_t qw, ww;  // this range's qualifying / window line counts
 };
 
+// Granules of the previous bucket, loaded (per lane of the gather waves) at
+// the start of the next bucket's scan so the exchange round trip overlaps the
+// streaming pass; finish() re-polls only lanes whose tag was not yet current.
+struct Prefetch {};  // (kept in LDS: Lds::pf, filled by LDS-DMA)
+
 __device__ __forceinline__ uint32_t bitlen(uint32_t x) { return x ? 32u - __clz(x) : 0u; }
+
+// Workgroup-uniform values read from memory or LDS: move them to SGPRs (the
+// compiler cannot prove uniformity; VGPR copies would spill at 64 VGPRs, and
+// a scratch reload waits for every outstanding store of the wave).
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
 
 // Tree sum of one 16-float line held as a float4 by each lane of a quad
 // (lanes 0,1: floats 0..7; lanes 2,3: floats 8..15): p = |x_i| + |x_{i+4}|,
@@ -167,34 +186,62 @@ __device__ __forceinline__ void emit_line(const BucketDesc &d, bool vec, uint32_
 struct Ctx {
     const BatchArgs &A;
     Lds &L;
-    uint32_t G, w, tid, lane, wave;
+    uint32_t G, w, wave;
     uint32_t nbar;  // grid-barrier rounds used so far (the same in every workgroup)
+    bool probe;     // STAGE 4: sub-phase stamps of the probed bucket
+
+    // STAGE 4 only: stamps[16*1024 + w*16 + k]
+    __device__ __forceinline__ void sub(uint32_t k) const {
+        if (probe && ftid() == 0) L.stamp[16 + k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
 
     __device__ __forceinline__ uint32_t tag(uint32_t b) const { return (A.epoch << 8) | b; }
-    __device__ __forceinline__ uint32_t range_lo(uint32_t nb) const { return (uint32_t)((uint64_t)w * nb / G); }
-    __device__ __forceinline__ uint32_t range_len(uint32_t nb) const {
-        return (uint32_t)((uint64_t)(w + 1) * nb / G) - range_lo(nb);
+    // Fresh (opaque) thread / lane ids per phase: keeps the compiler from
+    // hoisting per-thread addresses of every phase out of the bucket loop into
+    // live registers (they would spill).
+    __device__ __forceinline__ uint32_t ftid() const {
+        uint32_t x = threadIdx.x;
+        asm volatile("" : "+v"(x));
+        return x;
     }
+    FillCtl *ctlp;    // control pointers, laundered per bucket iteration
+    uint64_t *candp;
+    uint32_t *failp;
+    __device__ __forceinline__ FillCtl *ctl() const { return ctlp; }
+    __device__ __forceinline__ uint64_t *cand() const { return candp; }
+    __device__ __forceinline__ uint32_t *fail() const { return failp; }
+    __device__ __forceinline__ uint32_t flane() const {
+        uint32_t x;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+        return x;
+    }
+    // Workgroup w's line range of a bucket (host-computed split, scalar math).
+    __device__ __forceinline__ uint32_t range_lo(const BucketDesc &d) const {
+        return w * d.per + (w < d.rem ? w : d.rem);
+    }
+    __device__ __forceinline__ uint32_t range_len(const BucketDesc &d) const { return d.per + (w < d.rem ? 1u : 0u); }
 
     // Last-arriver grid barrier: the workgroup whose arrival completes round r
     // writes every workgroup's own go word; each workgroup polls only its own.
     __device__ __forceinline__ void grid_sync() {
         const uint32_t r = ++nbar;
-        CallCtl *cc = &A.ctl->cc[A.epoch & 1u];
+        FillCtl *fc = ctl();
+        CallCtl *cc = &fc->cc[A.epoch & 1u];
         const uint64_t go = ((uint64_t)(A.epoch << 8) << 32) | r;
+        const uint32_t tid = ftid();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) L.dec[7] = __hip_atomic_fetch_add(&cc->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         if (L.dec[7] == r * G - 1) {
-            for (uint32_t i = tid; i < G; i += FWG) st_sc1(&A.ctl->slot[i].go, go);
+            for (uint32_t i = tid; i < G; i += FWG) st_sc1(&fc->slot[i].go, go);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
         if (tid == 0) {
-            for (uint32_t spins = 0; ld_sc1(&A.ctl->slot[w].go) != go; ++spins) {
+            for (uint32_t spins = 0; ld_sc1(&fc->slot[w].go) != go; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spins > (1u << 24)) { atomicOr(A.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+                if (spins > (1u << 24)) { atomicOr(fail(), (uint32_t)FAIL_SPIN_TIMEOUT); break; }
             }
         }
         __syncthreads();
@@ -203,23 +250,32 @@ struct Ctx {
 
 // ---- scan(b): stream this workgroup's range of bucket b ----
 template <int STAGE, bool LDS_SUMS>
-__device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b) {
+__device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b, Prefetch &pf) {
     const BucketDesc &d = C.A.bk[b];
     Lds &L = C.L;
-    const uint32_t par = b & 1u;
-    const uint32_t L0 = C.range_lo(d.nb), nl = C.range_len(d.nb);
+    if (b >= LA && C.wave * 64 < C.G) {
+        // The previous bucket's granules, fetched global -> LDS (no registers)
+        // as the oldest load of this scan, so the exchange round trip overlaps
+        // the streaming pass; finish() re-polls only stale lanes.
+        const uint32_t v = C.wave * 64 + C.flane();
+        const uint64_t *src = &C.ctl()->gran[b - LA][v < C.G ? v : 0][0];
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src), &L.pf[C.wave * 64], 16, 0,
+                                         16 /* sc1 */);
+    }
+    const uint32_t par = b % NBUF;
+    const uint32_t L0 = C.range_lo(d), nl = C.range_len(d);
     Carry cr;
     // Read before publishing this bucket's counts: workgroup 0 rewrites the
     // state only after it has seen every workgroup's counts.
-    cr.t = d.state->t;
-    cr.inc = d.state->inc;
+    cr.t = uni(d.state->t);
+    cr.inc = uni(d.state->inc);
     const float t = cr.t;
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > WIN ? tb - WIN : 0u;  // window [wlo, tb) just below t
-    if (C.tid == 0) L.nst[par] = 0;
+    if (C.ftid() == 0) L.nst[par] = 0;
     __syncthreads();
 
-    const uint32_t lane = C.lane, wave = C.wave, q = lane & 3;
+    const uint32_t lane = C.flane(), wave = C.wave, q = lane & 3;
     const uint32_t lane_line = wave * 16 + (lane >> 2);  // line of this lane in a step
     constexpr uint32_t STEP = FWG / 4;                   // lines per step
     const uint32_t nbatch = ((nl + STEP - 1) / STEP + SCAN_U - 1) / SCAN_U;
@@ -287,11 +343,11 @@ __device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b) {
             }
         }
     }
-    if (lane == 0) { L.cnt[par][wave] = cnt_w; L.cnt[par][FNW + wave] = win_w; }
+    if (lane == 0) { L.cnt[wave] = cnt_w; L.cnt[FNW + wave] = win_w; }
     __syncthreads();
     cr.qw = cr.ww = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < FNW; ++i) { cr.qw += L.cnt[par][i]; cr.ww += L.cnt[par][FNW + i]; }
+    for (uint32_t i = 0; i < FNW; ++i) { cr.qw += L.cnt[i]; cr.ww += L.cnt[FNW + i]; }
     // workgroup-uniform: keep the carry in SGPRs across the next scan
     cr.qw = __builtin_amdgcn_readfirstlane(cr.qw);
     cr.ww = __builtin_amdgcn_readfirstlane(cr.ww);
@@ -299,10 +355,12 @@ __device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b) {
         if (cnt_w == 12345u) d.count_out[1] = win_w;  // keep the loop alive
         return cr;
     }
-    if (C.tid == 0) {
+    // published by the last wave: a wave's scratch reload or vmcnt(0) waits
+    // for its own outstanding stores, and the gather waves are the first ones
+    if (C.ftid() == FWG - 64) {
         const uint64_t tg = (uint64_t)C.tag(b) << 32;
-        st_sc1(&C.A.ctl->gran[b][C.w], tg | cr.qw);
-        st_sc1(&C.A.ctl->gran2[b][C.w], tg | cr.ww);
+        st_sc1(&C.ctl()->gran[b][C.w][0], tg | cr.qw);
+        st_sc1(&C.ctl()->gran[b][C.w][1], tg | cr.ww);
     }
     return cr;
 }
@@ -327,12 +385,12 @@ __device__ __forceinline__ void rank_emit(Ctx &C, const BucketDesc &d, const uin
     if (first_e >= total) return;
     const uint32_t tailpos = d.nb * 16;
     const uint64_t tail_comp = ((uint64_t)(~ford(tail_key)) << 32) | (uint64_t)tailpos;
-    for (uint32_t i = C.tid; i < total; i += FWG) L.cand[i] = i < nc_all ? ld_sc1(&cand[i]) : tail_comp;
+    for (uint32_t i = C.ftid(); i < total; i += FWG) L.cand[i] = i < nc_all ? ld_sc1(&cand[i]) : tail_comp;
     __syncthreads();
     for (uint32_t e = first_e + C.wave; e < total; e += C.G * FNW) {
         const uint64_t key = L.cand[e];
         uint32_t less = 0;
-        for (uint32_t j = C.lane; j < total; j += 64) less += L.cand[j] < key;
+        for (uint32_t j = C.flane(); j < total; j += 64) less += L.cand[j] < key;
         const uint32_t rank = wave_sum(less);
         const bool is_tail = add_tail && key == tail_comp;
         const bool tail_before = add_tail && tail_comp < key;
@@ -341,9 +399,9 @@ __device__ __forceinline__ void rank_emit(Ctx &C, const BucketDesc &d, const uin
         const uint64_t off = (uint64_t)cnt + 16ull * rank - (tail_before ? (uint64_t)(16u - d.tl) : 0ull);
         if (off < d.dst_len) {
             const uint32_t Ln = std::min<uint32_t>(len, d.dst_len - (uint32_t)off);
-            if (C.lane < Ln) {
-                d.val[off + C.lane] = d.src[(size_t)pos + C.lane];
-                d.idx[off + C.lane] = pos + C.lane + (uint32_t)d.idx_offset;
+            if (C.flane() < Ln) {
+                d.val[off + C.flane()] = d.src[(size_t)pos + C.flane()];
+                d.idx[off + C.flane()] = pos + C.flane() + (uint32_t)d.idx_offset;
             }
         }
     }
@@ -352,13 +410,13 @@ __device__ __forceinline__ void rank_emit(Ctx &C, const BucketDesc &d, const uin
 
 // ---- finish(b): exchange, regime, emission, AIMD; regime B heap fill ----
 template <int STAGE>
-__device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &cr) {
+__device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &cr, const Prefetch &pf) {
     const BucketDesc &d = C.A.bk[b];
     Lds &L = C.L;
-    FillCtl *ctl = C.A.ctl;
-    const uint32_t par = b & 1u;
-    const uint32_t G = C.G, w = C.w, tid = C.tid, lane = C.lane, wave = C.wave;
-    const uint32_t L0 = C.range_lo(d.nb), nl = C.range_len(d.nb);
+    FillCtl *ctl = C.ctl();
+    const uint32_t par = b % NBUF;
+    const uint32_t G = C.G, w = C.w, tid = C.ftid(), lane = C.flane(), wave = C.wave;
+    const uint32_t L0 = C.range_lo(d), nl = C.range_len(d);
     const bool lds_sums = nl <= LINES_B;
     const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.idx) |
                        reinterpret_cast<uintptr_t>(d.val)) & 15u) == 0;
@@ -367,27 +425,34 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > WIN ? tb - WIN : 0u;
     const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
-    BucketCtl *bc = &ctl->cc[C.A.epoch & 1u].bk[b];
-    uint64_t *cand = C.A.cand + (size_t)(b & 3u) * CAND_CAP;
+    auto bc = [&]() { return &C.ctl()->cc[C.A.epoch & 1u].bk[b]; };  // per use: not held live
+    uint64_t *cand = C.cand() + (size_t)(b & 3u) * CAND_CAP;
 
+    C.sub(1);
     // ---- count exchange: wave j gathers workgroups [64j, 64j+64) (one
     //      granule pair per lane, all in flight), re-polling only stale ones ----
     const uint32_t nsw = (G + 63) / 64;
     if (wave < nsw) {
         const uint32_t tg = C.tag(b);
         const uint32_t v = wave * 64 + lane;
-        uint64_t g = 0, g2 = 0;
-        bool pend = v < G;
+        const uint4 e = L.pf[v];  // prefetched during this bucket's successor's scan
+        uint64_t g = ((uint64_t)e.y << 32) | e.x, g2 = ((uint64_t)e.w << 32) | e.z;
+        bool pend = v < G && ((uint32_t)(g >> 32) != tg || (uint32_t)(g2 >> 32) != tg);
+        if (C.probe && lane == 0) atomicAdd(&L.stamp[16 + 8], (uint32_t)__popcll(__ballot(pend)));
+        uint32_t polls = 0;
         for (uint32_t spins = 0;; ++spins) {
+            if (!__any(pend)) break;
+            ++polls;
             if (pend) {
-                g = ld_sc1(&ctl->gran[b][v]);
-                g2 = ld_sc1(&ctl->gran2[b][v]);
+                g = ld_sc1(&ctl->gran[b][v][0]);
+                g2 = ld_sc1(&ctl->gran[b][v][1]);
                 pend = (uint32_t)(g >> 32) != tg || (uint32_t)(g2 >> 32) != tg;
             }
             if (!__any(pend)) break;
-            __builtin_amdgcn_s_sleep(2);
-            if (spins > (1u << 22)) { atomicOr(C.A.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+            __builtin_amdgcn_s_sleep(1);
+            if (spins > (1u << 22)) { atomicOr(C.fail(), (uint32_t)FAIL_SPIN_TIMEOUT); break; }
         }
+        if (C.probe && lane == 0) atomicMax(&L.stamp[16 + 9], polls);
         const uint32_t c = v < G ? (uint32_t)g : 0u, cw = v < G ? (uint32_t)g2 : 0u;
         const uint32_t tot = wave_sum(c), wtot = wave_sum(cw);
         const uint32_t bef = wave_sum(v < w ? c : 0u), wbef = wave_sum(v < w ? cw : 0u);
@@ -406,9 +471,14 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
         Wbef += L.xch[j][2];
         Wtot += L.xch[j][3];
     }
+    P = uni(P);
+    Qtot = uni(Qtot);
+    Wbef = uni(Wbef);
+    Wtot = uni(Wtot);
     __syncthreads();
     if (STAGE == 2) return Defer{};
 
+    C.sub(2);
     // ---- regime (identical in every workgroup) ----
     const uint32_t lim = kb + (r ? 1u : 0u);
     const uint32_t c0 = Qtot >= lim ? d.dst_len : 16u * Qtot;
@@ -419,6 +489,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
         const float *tp = d.src + (size_t)d.nb * 16;
         float s = 0.f;
         for (uint32_t i = 0; i < d.tl; ++i) s += tp[i];
+        s = uni(s);
         if (s * 16.0f >= t * (float)d.tl) ct = std::min(d.dst_len - c0, d.tl);
         else { tail_cand = true; tail_key = s * 16.0f / (float)d.tl; }
     }
@@ -507,6 +578,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
         }
     }
 
+    C.sub(3);
     // ---- tail, AIMD, count (workgroup 0) ----
     if (w == 0 && tid == 0) {
         if (ct) {
@@ -521,6 +593,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
         d.state->init = 1;
         *d.count_out = (uint32_t)std::min<uint64_t>(d.dst_len, (uint64_t)d.nb * 16 + d.tl);
     }
+    C.sub(4);
     if (!regimeB) return Defer{};
 
     // ---- heap fill = top candidates by (sum desc, position asc) ----
@@ -543,24 +616,24 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
         }
         __syncthreads();
         for (uint32_t i = tid; i < HBINS; i += FWG)
-            if (L.hist[i]) atomicAdd(&bc->hist[0][i], L.hist[i]);
+            if (L.hist[i]) atomicAdd(&bc()->hist[0][i], L.hist[i]);
         C.grid_sync();
         uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
         bool ovf = true;
         for (;;) {
             // locate the bin holding rank `need` (1-based) counting down from hi
             const uint32_t need = M - above;
-            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&bc->hist[lvl][tid]) : 0u;
+            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&bc()->hist[lvl][tid]) : 0u;
             uint32_t total;
             const uint32_t before = blk_excl_scan<FNW>(cbin, L.sh, &total);
             if (tid == 0) { L.dec[2] = 0xffffffffu; L.dec[3] = 0; L.dec[4] = 0; }
             __syncthreads();
             if (tid < HBINS && need > before && need <= before + cbin) { L.dec[2] = tid; L.dec[3] = before; L.dec[4] = cbin; }
             __syncthreads();
-            const uint32_t bstar = L.dec[2], cum = L.dec[3], hb = L.dec[4];
+            const uint32_t bstar = uni(L.dec[2]), cum = uni(L.dec[3]), hb = uni(L.dec[4]);
             __syncthreads();
             if (bstar == 0xffffffffu) {  // histogram does not reach `need`: collect all
-                if (tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_LEVELS);
+                if (tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_LEVELS);
                 mode = 1; blo = 0;
                 break;
             }
@@ -568,7 +641,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
                 above += cum;
                 const uint64_t width = (uint64_t)(HBINS - 1) << s;
                 if ((uint64_t)hi < width) {
-                    if (tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_LEVELS);
+                    if (tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_LEVELS);
                     mode = 1; blo = 0;
                     break;
                 }
@@ -589,7 +662,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
                 s = s >= 10 ? s - 10 : 0;
             }
             if (++lvl >= MAX_LEVELS) {
-                if (tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_LEVELS);
+                if (tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_LEVELS);
                 mode = 1; blo = lo;
                 break;
             }
@@ -601,7 +674,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
             }
             __syncthreads();
             for (uint32_t i = tid; i < HBINS; i += FWG)
-                if (L.hist[i]) atomicAdd(&bc->hist[lvl][i], L.hist[i]);
+                if (L.hist[i]) atomicAdd(&bc()->hist[lvl][i], L.hist[i]);
             C.grid_sync();
         }
     }
@@ -632,7 +705,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
                 base = run;
                 run += n_here;
             } else {
-                if (tid == 0) L.dec[7] = atomicAdd(&bc->cand_n, n_here);
+                if (tid == 0) L.dec[7] = atomicAdd(&bc()->cand_n, n_here);
                 __syncthreads();
                 base = L.dec[7];
                 __syncthreads();
@@ -645,6 +718,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
             if (tid == 0) st_sc1(&ctl->wg_ties[b & 3u][w], my_ties);
         }
     }
+    C.sub(5);
     if (mode == 1) {
         // The common case: publish "candidates written" and rank the set
         // after the next bucket's scan (rank_deferred), when every workgroup's
@@ -690,9 +764,9 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
                 emit_line(d, false, tailpos, (uint32_t)off, std::min<uint32_t>(d.tl, d.dst_len - (uint32_t)off));
         }
     }
-    uint32_t nc_all = ld_acq_relaxed(&bc->cand_n);
+    uint32_t nc_all = uni(ld_acq_relaxed(&bc()->cand_n));
     if (nc_all > CAND_CAP) {
-        if (w == 0 && tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_CAND_OVERFLOW);
+        if (w == 0 && tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_CAND_OVERFLOW);
         nc_all = CAND_CAP;
     }
     rank_emit(C, d, cand, cnt, nc_all, tail_in_greater && nc_all < CAND_CAP, tail_key);
@@ -712,24 +786,24 @@ __device__ __forceinline__ void rank_deferred(Ctx &C, const Defer &D) {
     const uint32_t nsw = (C.G + 63) / 64;
     if (C.wave < nsw) {
         const uint32_t tg = C.tag(D.b);
-        const uint32_t v = C.wave * 64 + C.lane;
+        const uint32_t v = C.wave * 64 + C.flane();
         bool pend = v < C.G;
         for (uint32_t spins = 0;; ++spins) {
-            if (pend) pend = (uint32_t)(ld_sc1(&C.A.ctl->cdone[D.b][v]) >> 32) != tg;
+            if (pend) pend = (uint32_t)(ld_sc1(&C.ctl()->cdone[D.b][v]) >> 32) != tg;
             if (!__any(pend)) break;
             __builtin_amdgcn_s_sleep(2);
-            if (spins > (1u << 22)) { atomicOr(C.A.fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+            if (spins > (1u << 22)) { atomicOr(C.fail(), (uint32_t)FAIL_SPIN_TIMEOUT); break; }
         }
     }
     __syncthreads();
     uint32_t nc_all = D.nc;
-    if (nc_all == 0xffffffffu) nc_all = ld_acq_relaxed(&C.A.ctl->cc[C.A.epoch & 1u].bk[D.b].cand_n);
+    if (nc_all == 0xffffffffu) nc_all = uni(ld_acq_relaxed(&C.ctl()->cc[C.A.epoch & 1u].bk[D.b].cand_n));
     if (nc_all > CAND_CAP) {
-        if (C.tid == 0) atomicOr(C.A.fail, (uint32_t)FAIL_CAND_OVERFLOW);
+        if (C.ftid() == 0) atomicOr(C.fail(), (uint32_t)FAIL_CAND_OVERFLOW);
         nc_all = CAND_CAP;
     }
     (void)L;
-    rank_emit(C, d, C.A.cand + (size_t)(D.b & 3u) * CAND_CAP, D.cnt, nc_all, D.tail_cand && nc_all < CAND_CAP,
+    rank_emit(C, d, C.cand() + (size_t)(D.b & 3u) * CAND_CAP, D.cnt, nc_all, D.tail_cand && nc_all < CAND_CAP,
               D.tail_key);
 }
 
@@ -742,39 +816,55 @@ __device__ __forceinline__ void rank_deferred(Ctx &C, const Defer &D) {
 template <int STAGE>
 __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
     __shared__ Lds L;
-    Ctx C{A, L, gridDim.x, blockIdx.x, threadIdx.x, __lane_id(), (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), 0};
+    Ctx C{A, L, gridDim.x, blockIdx.x, (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), 0,
+          false, A.ctl, A.cand, A.fail};
+    // STAGE 4: stamps go to LDS (a global store here would make the wave's
+    // next vmcnt wait include its write-back) and are flushed at the end
     auto stamp = [&](uint32_t k) {
-        if (STAGE == 4 && C.tid == 0 && k < 16)
-            A.stamps[C.w * 16 + k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        if (STAGE == 4 && C.ftid() == 0 && k < 16) L.stamp[k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     };
+    if (STAGE == 4 && C.ftid() < 32) L.stamp[C.ftid()] = 0;
     stamp(15);
-    if (STAGE == 4 && C.tid == 0)
-        A.stamps[C.w * 16 + 14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
-
+    if (STAGE == 4 && C.ftid() == 0) L.stamp[14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
     {  // zero the next call's per-call counters (this call never touches them)
         uint32_t *z = reinterpret_cast<uint32_t *>(&A.ctl->cc[(A.epoch + 1) & 1u]);
         constexpr uint32_t words = sizeof(CallCtl) / 4;
         const uint32_t per = (words + C.G - 1) / C.G;
         const uint32_t z0 = C.w * per, z1 = std::min(words, z0 + per);
-        for (uint32_t i = z0 + C.tid; i < z1; i += FWG) st_sc1(z + i, 0u);
+        for (uint32_t i = z0 + C.ftid(); i < z1; i += FWG) st_sc1(z + i, 0u);
     }
-    // software pipeline: scan(b) | finish(b-1) | deferred rank of b-2
-    Carry prev{}, cur{};  // scan results of bucket b-1 and b (no indexed locals: no scratch)
-    Defer pend{};         // regime-B set of bucket b-2 awaiting its rank-and-emit
-    for (uint32_t b = 0; b <= A.nbk + 1; ++b) {
+    // software pipeline: scan(b) | finish(b-LA) | deferred rank of b-LA-1
+    static_assert(LA == 2, "carry rotation below is written for LA == 2");
+    Carry ca{}, cb{}, cur{};  // scan results of buckets b-2, b-1, b (no indexed locals: no scratch)
+    Defer pend{};             // regime-B set awaiting its rank-and-emit
+    Prefetch pf{};            // granules of bucket b-LA, loaded during scan(b) (into Lds::pf)
+    for (uint32_t b = 0; b <= A.nbk + LA; ++b) {
+        // opaque per iteration: addresses derived from the workgroup id are
+        // recomputed (scalar) instead of hoisted into live vector registers
+        asm volatile("" : "+s"(C.w), "+s"(C.G), "+s"(C.ctlp), "+s"(C.candp), "+s"(C.failp));
         if (b < A.nbk) {
             // ranges beyond LINES_B keep their line sums in global scratch
-            if (C.range_len(A.bk[b].nb) <= LINES_B) cur = scan_bucket<STAGE, true>(C, b);
-            else cur = scan_bucket<STAGE, false>(C, b);
+            if (C.range_len(A.bk[b]) <= LINES_B) cur = scan_bucket<STAGE, true>(C, b, pf);
+            else cur = scan_bucket<STAGE, false>(C, b, pf);
             if (b < 7) stamp(2 * b);
         }
         if (STAGE == 1 || STAGE == 3) continue;
         Defer dn{};
-        if (b > 0 && b <= A.nbk) dn = finish_bucket<STAGE>(C, b - 1, prev);
+        C.probe = STAGE == 4 && b == 2 + LA;
+        if (b >= LA && b - LA < A.nbk) dn = finish_bucket<STAGE>(C, b - LA, ca, pf);
+        C.sub(6);
         rank_deferred(C, pend);
-        if (b > 0 && b - 1 < 7) stamp(2 * (b - 1) + 1);
+        C.sub(7);
+        C.probe = false;
+        if (b >= LA && b - LA < 7) stamp(2 * (b - LA) + 1);
         pend = dn;
-        prev = cur;
+        ca = cb;
+        cb = cur;
+    }
+    if (STAGE == 4) {
+        __syncthreads();
+        if (C.ftid() < 16) A.stamps[C.w * 16 + C.ftid()] = L.stamp[C.ftid()];
+        else if (C.ftid() < 32) A.stamps[16 * 1024 + C.w * 16 + C.ftid() - 16] = L.stamp[C.ftid()];
     }
 }
 
@@ -821,6 +911,10 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     const uint32_t G = std::max<uint32_t>(
         1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, (max_nb + 1023) / 1024),
                               MAX_FILL_WG));
+    for (uint32_t i = 0; i < a.nb; ++i) {
+        A.bk[i].per = A.bk[i].nb / G;
+        A.bk[i].rem = A.bk[i].nb % G;
+    }
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     switch (dbg_stage) {

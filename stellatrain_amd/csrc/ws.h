@@ -52,8 +52,9 @@ struct alignas(128) WgSlot {
 struct FillCtl {
     CallCtl cc[2];                     // [epoch parity]
     uint32_t wg_ties[4][MAX_FILL_WG];  // [bucket % 4] regime-B ties per workgroup
-    uint64_t gran[MAX_BATCH][MAX_FILL_WG];   // {tag:32 | count:32}, never zeroed
-    uint64_t gran2[MAX_BATCH][MAX_FILL_WG];  // {tag:32 | window count:32}
+    // per bucket and workgroup: [0] = {tag:32 | qualifying lines:32},
+    // [1] = {tag:32 | window lines:32}; 16 B so one lane fetches both
+    uint64_t gran[MAX_BATCH][MAX_FILL_WG][2];
     uint64_t cdone[MAX_BATCH][MAX_FILL_WG];  // {tag:32 | 0}: regime-B candidates written
     WgSlot slot[MAX_FILL_WG];
 };
