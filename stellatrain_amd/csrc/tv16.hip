@@ -594,7 +594,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
         *d.count_out = (uint32_t)std::min<uint64_t>(d.dst_len, (uint64_t)d.nb * 16 + d.tl);
     }
     C.sub(4);
-    if (!regimeB) return Defer{};
+    if (!regimeB || STAGE == 5) return Defer{};
 
     // ---- heap fill = top candidates by (sum desc, position asc) ----
     const uint32_t rem = d.dst_len - cnt;
@@ -812,7 +812,7 @@ __device__ __forceinline__ void rank_deferred(Ctx &C, const Defer &D) {
 // 3 = plain streaming read (calibration); 4 = full codec + per-workgroup
 // s_memrealtime stamps: stamps[w*16 + 15] at start, [w*16 + 2b] after scan(b),
 // [w*16 + 2b + 1] after finish(b) and the deferred rank of b-1 (b < 7),
-// [w*16 + 14] = XCC id.
+// [w*16 + 14] = XCC id; 5 = full codec without the regime-B heap fill.
 template <int STAGE>
 __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
     __shared__ Lds L;
@@ -922,6 +922,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         case 2: tv16_batch<2><<<G, FWG, 0, s>>>(A); break;
         case 3: tv16_batch<3><<<G, FWG, 0, s>>>(A); break;
         case 4: tv16_batch<4><<<G, FWG, 0, s>>>(A); break;
+        case 5: tv16_batch<5><<<G, FWG, 0, s>>>(A); break;
         default: tv16_batch<0><<<G, FWG, 0, s>>>(A); break;
     }
     if (a.ev) {

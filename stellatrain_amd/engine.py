@@ -40,13 +40,16 @@ def api_numel(n: int, ratio: float) -> int:
 
 def owner_of(sizes, world: int) -> list[int]:
     """Key-affine bucket placement for multi-GPU runs: greedy
-    bytes-balancing in bucket order; a bucket's AIMD state lives on its owner."""
+    longest-first bytes balancing (largest bucket to the least-loaded rank,
+    ties by rank and bucket order); deterministic, so a key always lands on the
+    same rank and its AIMD state stays resident there."""
     load = [0] * world
-    out = []
-    for s in sizes:
+    out = [0] * len(sizes)
+    order = sorted(range(len(sizes)), key=lambda i: (-int(sizes[i]), i))
+    for i in order:
         g = min(range(world), key=lambda r: (load[r], r))
-        load[g] += int(s)
-        out.append(g)
+        load[g] += int(sizes[i])
+        out[i] = g
     return out
 
 

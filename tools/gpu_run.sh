@@ -37,7 +37,7 @@ for s in "$@"; do
                 -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 16 --warmup 4 --profile-steps 4 --no-cpu-baseline ;;
         pmc_write) step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
                 -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 16 --warmup 4 --profile-steps 4 --no-cpu-baseline ;;
-        prof_s1|prof_s2|prof_s3)
+        prof_s1|prof_s2|prof_s3|prof_s5)
             export STG_DEBUG_TV16_STAGE=${s#prof_s}
             step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$s" -o run \
                 -- python3 bench.py --steps 50 --warmup 8 --no-cpu-baseline
