@@ -1,0 +1,280 @@
+#!/usr/bin/env python3
+"""Secondary measurements for BASELINE.json configs 2-5 (GPU box).
+
+bench.py carries the headline line (thresholdv16, 64 MiB, k=1%).  This tool
+times the other configs on one GPU and prints one JSON line per measurement:
+
+  C2  top-k k=1% on 64 MiB buckets ("topk" bug-compatible and "topk_exact"),
+      device resident;
+  C3  threshold-v k=0.1% on 256 MiB buckets, device resident, and host
+      inclusive: src in pinned host memory (the reference's cudaHostRegister'd
+      shm, shm_manager.cpp:92), H2D + codec + D2H of the (idx, val) stream,
+      serial (stg_codec_compress_host) and with the H2D of bucket i+1
+      overlapped with the codec on bucket i (two streams);
+  C4  the 1024-bucket stream (256 KiB..64 MiB, log-uniform, seeded) through
+      thresholdv16 batches of 16, device resident;
+  C5  compress -> MERGE decompress -> sparse SGD (momentum 0.9) on 64 MiB;
+  E2E thresholdv16 64 MiB host-inclusive (serial and overlapped).
+
+Every device timing rotates over >= 512 MB of distinct buckets so the 256 MB
+Infinity Cache cannot serve the reads.  GB/s = dense fp32 bytes in / time.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PEAK = 8000.0
+
+
+def emit(d):
+    print(json.dumps(d), flush=True)
+
+
+def fill(lib, t, seed, stream):
+    from stellatrain_amd._capi import check
+    check(lib.stg_synth_fill_device(C.c_void_p(t.data_ptr()), t.numel(), seed, 0, 0, C.c_void_p(stream)))
+
+
+def bufs_for(torch, lib, dev, n, count, stream, base_seed=0):
+    from stellatrain_amd.synth import seed_for
+    out = []
+    for i in range(count):
+        t = torch.empty(n, dtype=torch.float32, device=dev)
+        fill(lib, t, seed_for(base_seed + i, 0), stream)
+        out.append(t)
+    return out
+
+
+def time_device(torch, comp, method, mib, ratio, calls, warmup, keys):
+    """One key per buffer; rotate over >= 512 MB."""
+    from stellatrain_amd import merge_numel
+    from stellatrain_amd._capi import lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = mib * (1 << 20) // 4
+    k = merge_numel(n, ratio)
+    nbuf = max(keys, math.ceil(512 / mib) + 1)
+    bufs = bufs_for(torch, lib(), dev, n, nbuf, st.cuda_stream, 100)
+    idx = torch.zeros(k, dtype=torch.int32, device=dev)
+    val = torch.zeros(k, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    keyb = [f"{i % keys}@weight".encode() for i in range(nbuf)]
+    # threshold-v keys by src pointer: every buffer is its own key there
+    for i in range(nbuf):
+        comp.compress_raw(keyb[i], bufs[i].data_ptr(), n, k, idx.data_ptr(), k, val.data_ptr(), cnt.data_ptr(),
+                          st.cuda_stream)
+    for i in range(warmup):
+        j = i % nbuf
+        comp.compress_raw(keyb[j], bufs[j].data_ptr(), n, k, idx.data_ptr(), k, val.data_ptr(), cnt.data_ptr(),
+                          st.cuda_stream)
+    torch.cuda.synchronize()
+    comp.set_timing(True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for i in range(calls):
+        j = i % nbuf
+        comp.compress_raw(keyb[j], bufs[j].data_ptr(), n, k, idx.data_ptr(), k, val.data_ptr(), cnt.data_ptr(),
+                          st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    (k0, k1, kall), launches = comp.get_timing()
+    comp.set_timing(False)
+    comp.check_device()
+    us = ms * 1e3 / calls
+    alg = 4.0 * n + 8.0 * k
+    return {"config": f"{method} {mib} MiB k={k}", "n": n, "k": k, "us_per_call": round(us, 2),
+            "GBps_dense_in": round(4.0 * n / us / 1e3, 1),
+            "alg_GBps": round(alg / us / 1e3, 1), "frac_hbm_peak": round(alg / us / 1e3 / PEAK, 4),
+            "kernel_us": {"main": round(k0 * 1e3 / max(launches, 1), 2), "second": round(k1 * 1e3 / max(launches, 1), 2),
+                          "call": round(kall * 1e3 / max(launches, 1), 2)},
+            "count": int(cnt.item()), "rotating_buffers": nbuf}
+
+
+def host_inclusive(torch, method, mib, ratio, calls):
+    """Serial compress_host from pinned memory, then the overlapped pipeline."""
+    from stellatrain_amd import make_compressor, merge_numel
+    from stellatrain_amd.synth import seed_for, synth
+    dev = torch.device("cuda", 0)
+    n = mib * (1 << 20) // 4
+    k = merge_numel(n, ratio)
+    nb = 4
+    host = [torch.from_numpy(synth(n, seed_for(200 + i, 0))).pin_memory() for i in range(nb)]
+    oi = np.zeros(k, np.uint32)
+    ov = np.zeros(k, np.float32)
+    comp = make_compressor(method)
+    for i in range(nb):
+        comp.compress(f"{i}@w", host[i].numpy(), k, oi, ov)
+    t0 = time.perf_counter()
+    for c in range(calls):
+        comp.compress(f"{c % nb}@w", host[c % nb].numpy(), k, oi, ov)
+    serial = (time.perf_counter() - t0) / calls
+    # overlapped: H2D of bucket c+1 on a copy stream while the codec runs on c
+    comp2 = make_compressor(method)
+    cs, ks = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    dbuf = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(2)]
+    didx = [torch.zeros(k, dtype=torch.int32, device=dev) for _ in range(2)]
+    dval = [torch.zeros(k, dtype=torch.float32, device=dev) for _ in range(2)]
+    hidx = [torch.zeros(k, dtype=torch.int32).pin_memory() for _ in range(2)]
+    hval = [torch.zeros(k, dtype=torch.float32).pin_memory() for _ in range(2)]
+    copied = [torch.cuda.Event() for _ in range(2)]
+    done = [torch.cuda.Event() for _ in range(2)]
+
+    def run(total):
+        with torch.cuda.stream(cs):
+            dbuf[0].copy_(host[0], non_blocking=True)
+            copied[0].record(cs)
+        for c in range(total):
+            p = c % 2
+            if c + 1 < total:
+                q = (c + 1) % 2
+                with torch.cuda.stream(cs):
+                    cs.wait_event(done[q])
+                    dbuf[q].copy_(host[(c + 1) % nb], non_blocking=True)
+                    copied[q].record(cs)
+            with torch.cuda.stream(ks):
+                ks.wait_event(copied[p])
+                comp2.compress_async(f"{c % nb}@w", dbuf[p], k, didx[p], dval[p])
+                hidx[p].copy_(didx[p], non_blocking=True)
+                hval[p].copy_(dval[p], non_blocking=True)
+                done[p].record(ks)
+        torch.cuda.synchronize()
+    run(nb)
+    t0 = time.perf_counter()
+    run(calls)
+    ovl = (time.perf_counter() - t0) / calls
+    # H2D alone (pinned -> device), the PCIe ceiling of this path
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for c in range(calls):
+        dbuf[0].copy_(host[c % nb], non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = (time.perf_counter() - t0) / calls
+    return {"config": f"{method} {mib} MiB k={k} host-inclusive", "n": n, "k": k,
+            "serial_us_per_call": round(serial * 1e6, 1), "serial_GBps_dense_in": round(4.0 * n / serial / 1e9, 2),
+            "overlapped_us_per_call": round(ovl * 1e6, 1), "overlapped_GBps_dense_in": round(4.0 * n / ovl / 1e9, 2),
+            "h2d_only_GBps": round(4.0 * n / h2d / 1e9, 2)}
+
+
+def c4_stream(torch, batches_timed):
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel
+    from stellatrain_amd._capi import lib
+    from stellatrain_amd.shard import ShardPlan, c4_sizes
+    from stellatrain_amd.synth import seed_for
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    sizes = c4_sizes()
+    plan = ShardPlan(sizes, 1)
+    ids = plan.local(0)
+    total = sum(sizes)
+    flat = torch.empty(total, dtype=torch.float32, device=dev)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    for i in ids:
+        seg = flat[offs[i]:offs[i + 1]]
+        fill(lib(), seg, seed_for(i, 0), st.cuda_stream)
+    ks = [merge_numel(n, 0.99) for n in sizes]
+    kt = sum(ks)
+    oidx = torch.zeros(kt, dtype=torch.int32, device=dev)
+    oval = torch.zeros(kt, dtype=torch.float32, device=dev)
+    koffs = np.concatenate([[0], np.cumsum(ks)]).astype(np.int64)
+    counts = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+    comp = ThresholdvCompressor16()
+    rows = [(plan.key(i).encode(), flat[offs[i]:].data_ptr(), sizes[i], ks[i], oidx[koffs[i]:].data_ptr(), ks[i],
+             oval[koffs[i]:].data_ptr(), counts.data_ptr() + 4 * i) for i in ids]
+    batches = [comp.bucket_array(rows[j:j + 16]) for j in range(0, len(rows), 16)]
+    nrows = [len(rows[j:j + 16]) for j in range(0, len(rows), 16)]
+
+    def sweep():
+        for arr, nb in zip(batches, nrows):
+            comp.compress_batch_raw(arr, nb, st.cuda_stream)
+    sweep()  # first calls
+    sweep()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(batches_timed):
+        sweep()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / batches_timed
+    comp.check_device()
+    assert bool((counts.cpu().numpy() == np.array(ks)).all())
+    return {"config": "C4 thresholdv16 k=1% stream of 1024 buckets 256 KiB-64 MiB (1 GPU)", "buckets": len(ids),
+            "bytes": 4 * total, "ms_per_sweep": round(el * 1e3, 3), "GBps_dense_in": round(4.0 * total / el / 1e9, 1),
+            "launches": len(batches)}
+
+
+def c5_round_trip(torch, steps):
+    from stellatrain_amd import SparseSGD, ThresholdvCompressor16, merge_numel, scatter_merge
+    from stellatrain_amd._capi import lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = 16 << 20
+    k = merge_numel(n, 0.99)
+    nb = 9
+    grads = bufs_for(torch, lib(), dev, n, nb, st.cuda_stream, 300)
+    params = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(nb)]
+    for i, p in enumerate(params):
+        fill(lib(), p, 777 + i, st.cuda_stream)
+    comp = ThresholdvCompressor16()
+    sgd = SparseSGD(lr=0.1, momentum=0.9)
+    idx = torch.zeros(k, dtype=torch.int32, device=dev)
+    val = torch.zeros(k, dtype=torch.float32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    oi = torch.empty(k, dtype=torch.int32, device=dev)
+    ov = torch.empty(k, dtype=torch.float32, device=dev)
+    oc = torch.empty(1, dtype=torch.int32, device=dev)
+
+    def step(s):
+        j = s % nb
+        comp.compress_async(f"{j}@w", grads[j], k, idx, val, count=cnt)
+        scatter_merge(idx, val, k, 1, n, out_idx=oi, out_val=ov, count=oc)
+        sgd.optimize_raw(params[j], f"{j}@w", ov, oi, grad_len=k, d_grad_len=oc)
+    for s in range(2 * nb):
+        step(s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for s in range(steps):
+        step(s)
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / steps
+    alg = 4.0 * n + 8.0 * k + 16.0 * k
+    return {"config": f"C5 thresholdv16 compress + decompress + SGD(m=0.9) 64 MiB k={k}", "us_per_step": round(us, 2),
+            "GBps_dense_in": round(4.0 * n / us / 1e3, 1), "alg_GBps": round(alg / us / 1e3, 1)}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--calls", type=int, default=48)
+    p.add_argument("--only", default="c2,c3,c4,c5,e2e")
+    a = p.parse_args()
+    import torch
+    from stellatrain_amd import make_compressor
+    only = set(a.only.split(","))
+    if "c2" in only:
+        for m in ("topk", "topk_exact"):
+            emit(time_device(torch, make_compressor(m), m, 64, 0.99, a.calls, 8, 9))
+    if "c3" in only:
+        emit(time_device(torch, make_compressor("thresholdv"), "thresholdv", 256, 0.999, a.calls, 8, 3))
+        emit(host_inclusive(torch, "thresholdv", 256, 0.999, 12))
+    if "e2e" in only:
+        emit(host_inclusive(torch, "thresholdv16", 64, 0.99, 24))
+    if "c4" in only:
+        emit(c4_stream(torch, 3))
+    if "c5" in only:
+        emit(c5_round_trip(torch, a.calls))
+
+
+if __name__ == "__main__":
+    main()

@@ -43,6 +43,7 @@ for s in "$@"; do
                 -- python3 bench.py --steps 50 --warmup 8 --no-cpu-baseline
             unset STG_DEBUG_TV16_STAGE ;;
         ubench) step ubench 300 python tools/ubench_read.py ;;
+        configs) step configs 500 python tools/bench_configs.py ;;
         sweep)
             for W in 1 2; do for S in 1 2; do for K in 8 16; do
                 export STG_TV16_WGPERCU=$W
