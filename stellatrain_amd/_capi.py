@@ -10,7 +10,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstg_codec.so")
+# STG_CODEC_LIB: an alternative in-tree build of the same sources (tuning
+# experiments, tools/gpu_run.sh); the default is the product library.
+LIB_PATH = os.environ.get("STG_CODEC_LIB") or os.path.join(_HERE, "libstg_codec.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "stg", "codec.h")
 
 STG_OK = 0

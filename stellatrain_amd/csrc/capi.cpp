@@ -50,8 +50,8 @@ struct Workspace {
     std::mutex mu;
     stg::DevWS d{};
     void *fixed = nullptr;
-    size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0;
-    uint32_t epoch = 0;  // thresholdv16 call counter (granule tags)
+    size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0, cap_desc = 0;
+    uint32_t epoch = 0;  // thresholdv16 call counter (hand-off tags)
     // device buffers of the host-memory entry point
     float *h_src = nullptr;
     size_t cap_src = 0;
@@ -66,6 +66,7 @@ struct Workspace {
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipFree(fixed);
         (void)hipFree(d.sums);
+        (void)hipFree(d.desc);
         (void)hipFree(d.tile_cnt);
         (void)hipFree(d.tile_aux);
         (void)hipFree(d.stage_pos);
@@ -112,6 +113,16 @@ struct Workspace {
         const size_t n = std::max<size_t>(need, cap + cap / 2);
         HIP_TRY(hipMalloc(&p, n * sizeof(T)));
         cap = n;
+        return STG_OK;
+    }
+
+    // thresholdv16 chunk descriptors: zeroed on (re)allocation, so no stale
+    // word carries a live call tag (epochs start at 1)
+    int ensure_desc(size_t n) {
+        if (n <= cap_desc) return STG_OK;
+        int rc;
+        if ((rc = grow(d.desc, cap_desc, n))) return rc;
+        HIP_TRY(hipMemset(d.desc, 0, cap_desc * sizeof(stg::ChunkDesc)));
         return STG_OK;
     }
 
@@ -281,19 +292,22 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     for (auto &b : grp) need += (b.n + 15) / 16 + 64;
     int rc;
     if ((rc = ws->ensure(need, 1, 1))) return rc;
-    size_t off = 0;
+    size_t off = 0, chunks = 0;
     for (auto &b : grp) {
         b.sums = ws->d.sums + off;
         off += (b.n + 15) / 16 + 64;
+        chunks += std::max<size_t>(1, (b.n / 16 + stg::TV16_CHUNK - 1) / stg::TV16_CHUNK);
     }
+    if ((rc = ws->ensure_desc(chunks))) return rc;
     std::array<hipEvent_t, 3> evs{};
     bool timed = false;
     if ((rc = h->take_events(&evs, &timed))) return rc;
-    // 24-bit call epochs tag every hand-off word ({epoch:24 | bucket:8});
-    // epoch parity selects the per-call counters.  On wrap, clear the block.
+    // 24-bit call epochs tag every hand-off word ({epoch:24 | kind:8});
+    // epoch parity selects the per-call counters.  On wrap, clear the blocks.
     if (++ws->epoch >= (1u << 24)) {
         ws->epoch = 1;
         HIP_TRY(hipMemsetAsync(ws->d.ctl, 0, sizeof(stg::FillCtl), s));
+        HIP_TRY(hipMemsetAsync(ws->d.desc, 0, ws->cap_desc * sizeof(stg::ChunkDesc), s));
     }
     stg::Tv16Launch a{};
     a.b = grp.data();
@@ -302,6 +316,7 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     a.ev = timed ? evs.data() : nullptr;
     a.epoch = ws->epoch;
     a.wg_per_cu = fused_wg_per_cu();
+    a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     FusedLane &lane = g_lanes[h->device & 63];
     std::lock_guard<std::mutex> lg(lane.mu);
     const size_t max_inflight = a.wg_per_cu == 1 ? 2 : 1;

@@ -12,24 +12,34 @@
 // lines in descending-sum order (heap fill).  AIMD: t *= 0.99 (in double) when
 // the scan ran dry, t += inc otherwise.
 //
-// One persistent launch per batch of buckets (tv16_batch): 1024-thread
-// workgroups (1 or 2 per CU, all co-resident), each owning a contiguous range
-// of every bucket's lines.  Per bucket b:
-//   scan(b)   stream the range once (a quad of lanes per line, DPP cross-lane
-//             adds in the AVX tree order), keep the line sums in LDS, stage the
-//             qualifying lines' data in LDS, count S >= t and the lines in a
-//             window just below t; publish both counts as tagged granules;
-//   finish(b) gather every workgroup's granules (one wave, all loads in
-//             flight), derive the regime, emit this range's qualifying lines
-//             with global rank < kb (+1 partial) from LDS; workgroup 0 writes
-//             the tail, the AIMD threshold and the count; regime B only: rank
-//             the window candidates (or run a radix descent when the window
-//             does not hold them) with last-arriver grid barriers and emit the
-//             heap fill in (sum desc, position asc) order.
-// The launch runs scan(b+1) before finish(b): bucket b's count exchange and
-// the streaming tail of its slowest workgroups hide behind the next bucket's
-// streaming pass.  A key's first call runs tv16_seq_sums + a radix select
-// (select.hip) before the launch.
+// One persistent launch per batch of buckets (tv16_batch).  The buckets are
+// cut into 2048-line chunks (128 KiB), taken in order by 1024-thread
+// workgroups (2 per CU, all co-resident) from a per-call counter, so fast
+// workgroups take more chunks and every dependency below points backward in
+// time.  The 16 waves of a workgroup are specialised:
+//
+//   14 streaming waves  scan chunk after chunk and never wait on another
+//             workgroup: stream the chunk once (a quad of lanes per line, DPP
+//             cross-lane adds in the AVX tree order), stage the qualifying
+//             lines' data in LDS with one ballot per 16-line step (their
+//             in-chunk order), list the lines in a window just below t, and
+//             count both; the last wave done with a chunk publishes its
+//             aggregate counts.  They stall only when NBUF chunks ahead of
+//             the finisher (LDS buffer sets in use).
+//   finisher wave  per chunk: decoupled look-back over the bucket's earlier
+//             chunks for the prefix counts, publish the inclusive prefix,
+//             emit the chunk's qualifying lines with rank < kb (+1 partial)
+//             straight from LDS, write its window list at its window offset;
+//             the bucket's last chunk decides the regime and writes the tail,
+//             the AIMD threshold, the count and the decision.
+//   ranker wave    per bucket decided regime B: wait for every chunk's window
+//             list, rank this workgroup's share of the set and emit it in
+//             (sum desc, position asc) order.  When the window does not hold
+//             the top M it runs a radix descent over the bucket's line sums
+//             with grid barriers among the rankers.
+//
+// A key's first call runs tv16_seq_sums + a radix select (select.hip) before
+// the launch.
 #include <algorithm>
 #include <cstdlib>
 
@@ -41,16 +51,38 @@ namespace {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
-constexpr uint32_t FWG = 1024;     // workgroup: 16 waves
+constexpr uint32_t FWG = 1024;      // workgroup: 16 waves
 constexpr uint32_t FNW = FWG / 64;
-constexpr uint32_t L1_SHIFT = 14;  // level-1 bin width in ulps below t (~0.2% of t)
-constexpr uint32_t LA = 2;         // pipeline lookahead: finish(b) runs after scan(b + LA)
-constexpr uint32_t NBUF = LA + 1;  // LDS buffer sets (line sums, staged lines) in flight
-constexpr uint32_t LINES_B = 2048; // line sums kept in LDS per workgroup and buffer set
-constexpr uint32_t STAGE_B = 88;   // qualifying lines staged in LDS per workgroup and buffer set
-constexpr uint32_t SCAN_U = 8;     // float4 per lane per load batch
-constexpr uint32_t MAX_J = LINES_B / FWG;
-constexpr uint32_t WIN = 1u << 17; // regime-B window below t, in ulps (~1.6% of t)
+constexpr uint32_t NS = FNW - 2;    // streaming waves 0..13
+constexpr uint32_t FIN = NS;        // wave 14: finisher
+constexpr uint32_t RNK = NS + 1;    // wave 15: ranker (regime-B heap fill)
+static_assert(RNK == FNW - 1, "one streaming group, one finisher, one ranker");
+#ifndef STG_TV16_NBUF
+#define STG_TV16_NBUF 4
+#endif
+#ifndef STG_TV16_SCAN_D
+#define STG_TV16_SCAN_D 3
+#endif
+constexpr uint32_t NBUF = STG_TV16_NBUF;  // LDS buffer sets (slots) in flight per workgroup
+constexpr uint32_t CIDR = 2 * NBUF;       // chunk-id ring
+constexpr uint32_t MAX_STEPS = TV16_CHUNK / 16;  // wave steps (16 lines) of a chunk
+constexpr uint32_t STAGE_B = 88;    // qualifying lines staged in LDS per slot (~20 expected at 1%)
+constexpr uint32_t WL_B = 64;       // window candidates listed in LDS per slot
+#ifndef STG_TV16_RK
+#define STG_TV16_RK 64
+#endif
+constexpr uint32_t RK = STG_TV16_RK; // rankers per regime-B bucket (window path)
+constexpr uint32_t WBINS = 1024;    // window-path counting sort: bins over the top 10 key bits
+constexpr uint32_t GB = 512;        // chunk descriptors gathered per round trip (a 64 MiB bucket has 512)
+// float4 loads in flight per streaming wave: 2 x 14 x 64 x 16 B x SCAN_D per CU
+// (SCAN_D = 3: 84 KiB per CU, just over the ~72 KiB that hides an HBM miss;
+// deeper queues add latency to every exchange round trip -- Little's law)
+constexpr uint32_t SCAN_D = STG_TV16_SCAN_D;
+constexpr uint32_t MAXG = 512;      // workgroups per launch (2 per CU)
+constexpr uint32_t L1_SHIFT = 14;   // level-1 bin width in ulps below t (~0.2% of t)
+constexpr uint32_t WIN = 1u << 17;  // regime-B window below t, in ulps (~1.6% of t)
+constexpr uint32_t SPIN_MAX = 1u << 22;
+static_assert(SORT_CAP == MAX_BATCH * CAND_CAP, "one candidate slot per bucket of a launch");
 
 // ---------------------------------------------------------------------------
 // first call: sequential |x| sums per line, last partial line scaled by
@@ -93,10 +125,10 @@ struct BucketDesc {  // 80 bytes
     float *val;
     uint32_t *count_out;
     KeyState *state;
-    float *sums_g;  // line sums of ranges beyond LINES_B
+    float *sums_g;  // line sums, materialised by the rankers' rare paths
     uint32_t nb, tl, dst_len;
     int32_t idx_offset;
-    uint32_t per, rem;  // line ranges: workgroup w owns per + (w < rem) lines
+    uint32_t cs, nc;  // chunks [cs, cs + nc) of the launch's chunk sequence (nc >= 1)
     uint32_t pad[2];
 };
 
@@ -104,51 +136,71 @@ struct BatchArgs {
     BucketDesc bk[MAX_BATCH];
     uint32_t nbk;
     uint32_t epoch;  // 1 .. 2^24-1
+    uint32_t K;      // chunks in the launch
     FillCtl *ctl;
+    ChunkDesc *desc;
     uint64_t *cand;
     uint32_t *fail;
-    uint32_t *stamps;  // STAGE 4 diagnostics only
+    uint32_t *stamps;  // STAGE 4 diagnostics: 128 words per workgroup
 };
 
 // LDS of one workgroup (< 80 KiB: two workgroups per CU).
 struct Lds {
-    float sum[NBUF][LINES_B];       // line sums, by buffer set (bucket % NBUF)
-    float4 stage[NBUF][STAGE_B * 4];  // staged qualifying lines (64 B each)
+    // streaming waves -> finisher, by buffer set (slot % NBUF)
+    float4 stage[NBUF][STAGE_B * 4];     // staged qualifying lines (64 B each)
     uint32_t stage_line[NBUF][STAGE_B];
+    uint64_t qm[NBUF][MAX_STEPS];        // per wave step (16 lines): qualifying ballot (bits at quad leaders)
+    uint64_t wl[NBUF][WL_B];             // window candidates, composite keys
+    uint32_t nst[NBUF];                  // qualifying lines staged (slot counter)
+    uint32_t nwl[NBUF];                  // window candidates listed (slot counter)
+    uint32_t qcnt[NBUF];                 // qualifying lines of the chunk
+    uint32_t wcnt[NBUF];                 // window lines of the chunk
+    uint32_t sdone[NBUF];                // streaming waves done with the chunk
+    float tval[NBUF], incv[NBUF];        // the bucket's threshold state as scanned
+    uint32_t cid[CIDR];                  // chunk of slot j at [j % CIDR] (>= K: no more chunks)
+    uint32_t cseq;                       // slots whose chunk id is known
+    uint32_t fdone;                      // slots released by the finisher
+    // finisher
+    uint4 gb[GB];                        // gathered chunk descriptors (one piece of a bucket)
+    uint32_t wt[MAX_STEPS];              // exclusive popcounts of qm[par][]
+    // ranker
     union {
-        uint64_t cand[CAND_CAP];    // regime-B candidates (rank phase)
-        uint4 pf[MAX_FILL_WG];      // previous bucket's granules (scan -> finish)
+        uint64_t cand[CAND_CAP];         // rare path: candidate set (u64 composite keys)
+        uint32_t hist[HBINS];            // rare path: radix descent
+        struct {                         // window path: counting-sort rank of 32-bit keys
+            uint32_t key[CAND_CAP];      // the set, as gathered
+            uint32_t srt[CAND_CAP];      // the set sorted by top bits (bin order)
+            uint32_t bin[WBINS];         // bin counts -> bin ends
+            uint4 ent[64];               // this ranker's entries: {rank, pos, len, off}
+        } wr;
     };
-    uint64_t mask[MAX_J * FNW];
-    uint32_t hist[HBINS];
-    uint32_t wt[MAX_J * FNW + 1];
-    uint32_t sh[FNW + 1];
-    uint64_t sh64[FNW];
-    uint32_t dec[8];
-    uint32_t xch[FNW][4];           // count exchange partials per polling wave
-    uint32_t nst[NBUF];
-    uint32_t stamp[32];             // STAGE 4: timestamps, flushed at kernel end
-    uint32_t cnt[2 * FNW];          // per-wave counts of a scan
+    uint32_t stamp[128];                 // STAGE 4 diagnostics only
 };
-
-// Per-bucket values a workgroup carries from scan(b) to finish(b).
-struct Carry {
-    float t, inc;
-    uint32_t qw, ww;  // this range's qualifying / window line counts
-};
-
-// Granules of the previous bucket, loaded (per lane of the gather waves) at
-// the start of the next bucket's scan so the exchange round trip overlaps the
-// streaming pass; finish() re-polls only lanes whose tag was not yet current.
-struct Prefetch {};  // (kept in LDS: Lds::pf, filled by LDS-DMA)
 
 __device__ __forceinline__ uint32_t bitlen(uint32_t x) { return x ? 32u - __clz(x) : 0u; }
 
-// Workgroup-uniform values read from memory or LDS: move them to SGPRs (the
-// compiler cannot prove uniformity; VGPR copies would spill at 64 VGPRs, and
-// a scratch reload waits for every outstanding store of the wave).
+// Wave-uniform values read from memory or LDS: move them to SGPRs.
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ float uni(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
+
+// lane id, opaque to the compiler (not hoisted into a live register)
+__device__ __forceinline__ uint32_t flane() {
+    uint32_t x;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+    return x;
+}
+__device__ __forceinline__ uint64_t below_mask(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// LDS hand-offs between the waves of one workgroup: the writer drains its
+// LDS operations before the flag; LDS executes one wave's operations in order.
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t *p) {
+    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Tree sum of one 16-float line held as a float4 by each lane of a quad
 // (lanes 0,1: floats 0..7; lanes 2,3: floats 8..15): p = |x_i| + |x_{i+4}|,
@@ -163,6 +215,24 @@ __device__ __forceinline__ float quad_line_sum(const float4 v) {
     return h + dpp_f<QP_XOR2>(h);
 }
 
+// The same sum by one lane from memory (bit-identical: the same adds in the
+// same order; IEEE addition is commutative).
+__device__ __forceinline__ float lane_line_sum(const float *p) {
+    const float4 *p4 = reinterpret_cast<const float4 *>(p);
+    const float4 a = p4[0], b = p4[1], c = p4[2], e = p4[3];
+    const float lo = ((fabsf(a.x) + fabsf(b.x)) + (fabsf(a.y) + fabsf(b.y))) +
+                     ((fabsf(a.z) + fabsf(b.z)) + (fabsf(a.w) + fabsf(b.w)));
+    const float hi = ((fabsf(c.x) + fabsf(e.x)) + (fabsf(c.y) + fabsf(e.y))) +
+                     ((fabsf(c.z) + fabsf(e.z)) + (fabsf(c.w) + fabsf(e.w)));
+    return lo + hi;
+}
+
+// Composite heap-fill key: ascending order = (sum desc, position asc).
+__device__ __forceinline__ uint64_t cand_key(uint32_t u, uint32_t pos) {
+    return ((uint64_t)(~(u | 0x80000000u)) << 32) | (uint64_t)pos;
+}
+
+// One lane writes `len` (<= 16) pairs of the line at `pos` to slot `off`.
 __device__ __forceinline__ void emit_line(const BucketDesc &d, bool vec, uint32_t pos, uint32_t off, uint32_t len) {
     if (vec && len == 16) {
         const float4 *s4 = reinterpret_cast<const float4 *>(d.src + pos);
@@ -183,142 +253,153 @@ __device__ __forceinline__ void emit_line(const BucketDesc &d, bool vec, uint32_
     }
 }
 
+__device__ __forceinline__ bool aligned16(const BucketDesc &d) {
+    return ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.idx) |
+             reinterpret_cast<uintptr_t>(d.val)) & 15u) == 0;
+}
+
+// `n16` 16-byte words from global memory (read through to L2: sc1) into LDS
+// at `dst`, in chunks of 64 (the destination must hold whole chunks); waits.
+__device__ __forceinline__ void gather16(const void *src, uint32_t n16, void *dst) {
+    const uint32_t lane = flane();
+    for (uint32_t c = 0; c * 64 < n16; ++c) {
+        const uint32_t v = std::min(c * 64 + lane, n16 - 1);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const char *>(src) + (size_t)v * 16,
+                                         reinterpret_cast<char *>(dst) + c * 1024, 16, 0, 16 /* sc1 */);
+    }
+    vm_drain();
+}
+
 struct Ctx {
     const BatchArgs &A;
     Lds &L;
-    uint32_t G, w, wave;
-    uint32_t nbar;  // grid-barrier rounds used so far (the same in every workgroup)
-    bool probe;     // STAGE 4: sub-phase stamps of the probed bucket
-
-    // STAGE 4 only: stamps[16*1024 + w*16 + k]
-    __device__ __forceinline__ void sub(uint32_t k) const {
-        if (probe && ftid() == 0) L.stamp[16 + k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    }
-
-    __device__ __forceinline__ uint32_t tag(uint32_t b) const { return (A.epoch << 8) | b; }
-    // Fresh (opaque) thread / lane ids per phase: keeps the compiler from
-    // hoisting per-thread addresses of every phase out of the bucket loop into
-    // live registers (they would spill).
-    __device__ __forceinline__ uint32_t ftid() const {
-        uint32_t x = threadIdx.x;
-        asm volatile("" : "+v"(x));
-        return x;
-    }
-    FillCtl *ctlp;    // control pointers, laundered per bucket iteration
+    uint32_t G, w;
+    uint32_t nbar;  // ranker: grid-barrier rounds used so far (the same in every ranker)
+    FillCtl *ctlp;
     uint64_t *candp;
     uint32_t *failp;
-    __device__ __forceinline__ FillCtl *ctl() const { return ctlp; }
-    __device__ __forceinline__ uint64_t *cand() const { return candp; }
-    __device__ __forceinline__ uint32_t *fail() const { return failp; }
-    __device__ __forceinline__ uint32_t flane() const {
-        uint32_t x;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
-        return x;
-    }
-    // Workgroup w's line range of a bucket (host-computed split, scalar math).
-    __device__ __forceinline__ uint32_t range_lo(const BucketDesc &d) const {
-        return w * d.per + (w < d.rem ? w : d.rem);
-    }
-    __device__ __forceinline__ uint32_t range_len(const BucketDesc &d) const { return d.per + (w < d.rem ? 1u : 0u); }
+    bool stamping;  // STAGE 4
 
-    // Last-arriver grid barrier: the workgroup whose arrival completes round r
-    // writes every workgroup's own go word; each workgroup polls only its own.
+    __device__ __forceinline__ uint32_t tag(uint32_t kind) const { return (A.epoch << 8) | kind; }
+    __device__ __forceinline__ FillCtl *ctl() const { return ctlp; }
+    __device__ __forceinline__ CallCtl *cc() const { return &ctlp->cc[A.epoch & 1u]; }
+    __device__ __forceinline__ uint64_t *cand(uint32_t b) const { return candp + (size_t)b * CAND_CAP; }
+    __device__ __forceinline__ void fail(uint32_t bits) const { atomicOr(failp, bits); }
+    __device__ __forceinline__ void stamp(uint32_t slot, uint32_t v) const {
+        if (stamping && slot < 128 && flane() == 0) L.stamp[slot] = v ? v : (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
+    // bucket holding global chunk k (scalar search over <= 16 buckets)
+    __device__ __forceinline__ uint32_t bucket_of(uint32_t k) const {
+        uint32_t b = 0;
+        while (b + 1 < A.nbk && k >= A.bk[b + 1].cs) ++b;
+        return b;
+    }
+
+    // Grid barrier among the ranker waves (one per workgroup): the wave whose
+    // arrival completes round r writes every workgroup's own go word; each
+    // ranker polls only its own.  Bounded.
     __device__ __forceinline__ void grid_sync() {
         const uint32_t r = ++nbar;
         FillCtl *fc = ctl();
-        CallCtl *cc = &fc->cc[A.epoch & 1u];
         const uint64_t go = ((uint64_t)(A.epoch << 8) << 32) | r;
-        const uint32_t tid = ftid();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) L.dec[7] = __hip_atomic_fetch_add(&cc->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (L.dec[7] == r * G - 1) {
-            for (uint32_t i = tid; i < G; i += FWG) st_sc1(&fc->slot[i].go, go);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+        const uint32_t lane = flane();
+        vm_drain();
+        uint32_t old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(&cc()->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = uni(old);
+        if (old == r * G - 1) {
+            for (uint32_t i = lane; i < G; i += 64) st_sc1(&fc->slot[i].go, go);
+            vm_drain();
         }
-        if (tid == 0) {
-            for (uint32_t spins = 0; ld_sc1(&fc->slot[w].go) != go; ++spins) {
-                __builtin_amdgcn_s_sleep(1);
-                if (spins > (1u << 24)) { atomicOr(fail(), (uint32_t)FAIL_SPIN_TIMEOUT); break; }
-            }
+        for (uint32_t spins = 0; ld_sc1(&fc->slot[w].go) != go; ++spins) {
+            __builtin_amdgcn_s_sleep(1);
+            if (spins > SPIN_MAX) { if (lane == 0) fail(FAIL_SPIN_TIMEOUT); break; }
         }
-        __syncthreads();
     }
 };
 
-// ---- scan(b): stream this workgroup's range of bucket b ----
-template <int STAGE, bool LDS_SUMS>
-__device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b, Prefetch &pf) {
-    const BucketDesc &d = C.A.bk[b];
+constexpr uint32_t TAG_AGG = 1, TAG_DEC = 3, TAG_TIE = 4;
+constexpr uint32_t DEC_B = 1, DEC_WIN = 2, DEC_TAIL = 4;
+
+// ===========================================================================
+// streaming waves
+// ===========================================================================
+// scan of slot j = chunk k by streaming wave s: lines i = (s + NS*m)*16 +
+// lane/4 of the chunk, m = 0, 1, ...; SCAN_D float4 loads per lane in flight
+// through a buffer descriptor bounded to the chunk (lanes past it read zeros).
+template <int STAGE>
+__device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint32_t s) {
     Lds &L = C.L;
-    if (b >= LA && C.wave * 64 < C.G) {
-        // The previous bucket's granules, fetched global -> LDS (no registers)
-        // as the oldest load of this scan, so the exchange round trip overlaps
-        // the streaming pass; finish() re-polls only stale lanes.
-        const uint32_t v = C.wave * 64 + C.flane();
-        const uint64_t *src = &C.ctl()->gran[b - LA][v < C.G ? v : 0][0];
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src), &L.pf[C.wave * 64], 16, 0,
-                                         16 /* sc1 */);
+    const uint32_t par = j % NBUF;
+    if (j >= NBUF) {  // buffer set `par` is free once the finisher released slot j - NBUF
+        for (uint32_t spins = 0; lds_ld(&L.fdone) < j + 1 - NBUF; ++spins) {
+            __builtin_amdgcn_s_sleep(2);
+            if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+        }
     }
-    const uint32_t par = b % NBUF;
-    const uint32_t L0 = C.range_lo(d), nl = C.range_len(d);
-    Carry cr;
-    // Read before publishing this bucket's counts: workgroup 0 rewrites the
-    // state only after it has seen every workgroup's counts.
-    cr.t = uni(d.state->t);
-    cr.inc = uni(d.state->inc);
-    const float t = cr.t;
+    const uint32_t b = C.bucket_of(k);
+    const BucketDesc &d = C.A.bk[b];
+    const uint32_t c = k - d.cs;
+    const uint32_t L0 = c * TV16_CHUNK;
+    const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+    // Read before this chunk's counts are published: the bucket's last chunk
+    // rewrites the state only after every chunk's counts are in.
+    const float t = uni(d.state->t);
+    const uint32_t lane = flane(), q = lane & 3;
+    if (s == 0 && lane == 0) { L.tval[par] = t; L.incv[par] = uni(d.state->inc); }
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > WIN ? tb - WIN : 0u;  // window [wlo, tb) just below t
-    if (C.ftid() == 0) L.nst[par] = 0;
-    __syncthreads();
-
-    const uint32_t lane = C.flane(), wave = C.wave, q = lane & 3;
-    const uint32_t lane_line = wave * 16 + (lane >> 2);  // line of this lane in a step
-    constexpr uint32_t STEP = FWG / 4;                   // lines per step
-    const uint32_t nbatch = ((nl + STEP - 1) / STEP + SCAN_U - 1) / SCAN_U;
+    const uint32_t steps = (nl + 15) / 16;          // 16 lines per wave step
+    const uint32_t mine = steps > s ? (steps - s + NS - 1) / NS : 0u;
     uint32_t cnt_w = 0, win_w = 0;
-    // One batch of SCAN_U float4 per lane in flight; the 32 waves per CU
-    // supply the memory-level parallelism (tools/ubench_stream.hip: 1 x 1024
-    // threads/CU stream at ~4.0 TB/s, 2 x 1024 at ~5.4-5.8, nontemporal loads
-    // +5%).  Buffer loads (nt) through a descriptor bounded to the range: one
-    // 32-bit voffset per lane, the step in soffset, and lanes past the range
-    // read zeros from the hardware bounds check (no clamping code).
+    // nontemporal buffer loads; the whole offset goes in voffset so the
+    // hardware range check sees it
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(d.src + (size_t)L0 * 16), 0, nl * 64u, 0x00020000);
-    const uint32_t voff0 = lane_line * 64u + q * 16u;
-    for (uint32_t bt = 0; bt < nbatch; ++bt) {
-        // opaque per batch: keeps the compiler from hoisting SCAN_U line
-        // indices into live registers across the loop (they would spill)
-        uint32_t ll = lane_line;
-        asm volatile("" : "+v"(ll));
-        float4 v[SCAN_U];
+    const uint32_t lane_line = s * 16 + (lane >> 2);
+    auto load = [&](uint32_t m) -> float4 {
+        uint32_t voff = lane_line * 64u + q * 16u;
+        asm volatile("" : "+v"(voff));  // opaque: no hoisted per-step offsets
+        const u4v t4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + m * (NS * 1024u), 0, 2 /* nt */);
+        return make_float4(__uint_as_float(t4.x), __uint_as_float(t4.y), __uint_as_float(t4.z),
+                           __uint_as_float(t4.w));
+    };
+    // rolling pipeline: step m + SCAN_D is issued as soon as step m is consumed
+    float4 v[SCAN_D];
 #pragma unroll
-        for (uint32_t u = 0; u < SCAN_U; ++u) {
-            const u4v t4 = __builtin_amdgcn_raw_buffer_load_b128(
-                rsrc, voff0, (int)((bt * SCAN_U + u) * STEP * 64u), 2 /* nt */);
-            v[u] = make_float4(__uint_as_float(t4.x), __uint_as_float(t4.y), __uint_as_float(t4.z),
-                               __uint_as_float(t4.w));
-        }
+    for (uint32_t u = 0; u < SCAN_D; ++u) v[u] = load(u);
+    for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
 #pragma unroll
-        for (uint32_t u = 0; u < SCAN_U; ++u) {
-            const uint32_t i = (bt * SCAN_U + u) * STEP + ll;
+        for (uint32_t u = 0; u < SCAN_D; ++u) {
+            const float4 x = v[u];
+            uint32_t ll = lane_line;
+            asm volatile("" : "+v"(ll));
+            const uint32_t i = (m0 + u) * (NS * 16u) + ll;  // line within the chunk
             if (STAGE == 3) {
-                cnt_w += f2u(v[u].x + v[u].y + v[u].z + v[u].w) == 0x7f800001u;
+                cnt_w += f2u(x.x + x.y + x.z + x.w) == 0x7f800001u;
+                v[u] = load(m0 + u + SCAN_D);
                 continue;
             }
-            const float S = quad_line_sum(v[u]);  // the same in all four lanes of the quad
+            const float S = quad_line_sum(x);  // the same in all four lanes of the quad
+            v[u] = load(m0 + u + SCAN_D);
             const bool in = i < nl;
-            if (in && q == 0) {
-                if (LDS_SUMS) L.sum[par][i] = S;
-                else d.sums_g[L0 + i] = S;
-            }
+            const bool lead = in && q == 0;
             const uint32_t us = f2u(S);
             const bool qual = in && S >= t;
             const uint64_t bq = __ballot(qual && q == 0);
-            win_w += (uint32_t)__popcll(__ballot(in && q == 0 && us >= wlo && us < tb));
+            if (lane == 0 && i < nl) L.qm[par][i >> 4] = bq;
+            const bool win = lead && us >= wlo && us < tb;
+            const uint64_t bw = __ballot(win);
+            if (bw) {  // list the window candidates (composite keys)
+                win_w += (uint32_t)__popcll(bw);
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&L.nwl[par], (uint32_t)__popcll(bw));
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (win) {
+                    const uint32_t slot = base + (uint32_t)__popcll(bw & below_mask(flane()));
+                    if (slot < WL_B) L.wl[par][slot] = cand_key(us, (L0 + i) * 16);
+                }
+            }
             if (bq) {  // stage the qualifying lines (all four lanes of each quad)
                 cnt_w += (uint32_t)__popcll(bq);
                 uint32_t base = 0;
@@ -326,314 +407,510 @@ __device__ __forceinline__ Carry scan_bucket(Ctx &C, uint32_t b, Prefetch &pf) {
                 base = __builtin_amdgcn_readfirstlane(base);
                 if (qual) {
                     // qualifying quads before this one: bq has bits only at quad
-                    // leaders (multiples of 4), so leader p < this leader iff
-                    // p + 3 < lane -- a lane-count of bq << 3 (scalar shift)
+                    // leaders, so leader p < this leader iff p + 3 < lane
                     const uint64_t b3 = bq << 3;
                     const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi(
                         (uint32_t)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b3, 0u));
                     if (slot < STAGE_B) {
-                        // lane-in-quad recomputed here (a live copy would spill)
-                        uint32_t lq;
-                        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lq));
-                        lq &= 3u;
-                        L.stage[par][slot * 4 + lq] = v[u];
+                        const uint32_t lq = flane() & 3u;
+                        L.stage[par][slot * 4 + lq] = x;
                         if (lq == 0) L.stage_line[par][slot] = i;
                     }
                 }
             }
         }
     }
-    if (lane == 0) { L.cnt[wave] = cnt_w; L.cnt[FNW + wave] = win_w; }
-    __syncthreads();
-    cr.qw = cr.ww = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < FNW; ++i) { cr.qw += L.cnt[i]; cr.ww += L.cnt[FNW + i]; }
-    // workgroup-uniform: keep the carry in SGPRs across the next scan
-    cr.qw = __builtin_amdgcn_readfirstlane(cr.qw);
-    cr.ww = __builtin_amdgcn_readfirstlane(cr.ww);
-    if (STAGE == 1 || STAGE == 3) {
-        if (cnt_w == 12345u) d.count_out[1] = win_w;  // keep the loop alive
-        return cr;
+    if (lane == 0) {
+        if (cnt_w) atomicAdd(&L.qcnt[par], cnt_w);
+        if (win_w) atomicAdd(&L.wcnt[par], win_w);
     }
-    // published by the last wave: a wave's scratch reload or vmcnt(0) waits
-    // for its own outstanding stores, and the gather waves are the first ones
-    if (C.ftid() == FWG - 64) {
-        const uint64_t tg = (uint64_t)C.tag(b) << 32;
-        st_sc1(&C.ctl()->gran[b][C.w][0], tg | cr.qw);
-        st_sc1(&C.ctl()->gran[b][C.w][1], tg | cr.ww);
+    lds_drain();
+    uint32_t old = 0;
+    if (lane == 0) old = atomicAdd(&L.sdone[par], 1u);
+    if (STAGE != 1 && STAGE != 3 && uni(old) == NS - 1 && lane == 0) {
+        // the last streaming wave of the chunk publishes its aggregate at once
+        // (every other wave's count adds were drained before its sdone add)
+        const uint32_t aq = std::min(lds_ld(&L.qcnt[par]), 0xffffu), aw = std::min(lds_ld(&L.wcnt[par]), 0xffffu);
+        st_sc1(&C.A.desc[k].agg, ((uint64_t)C.tag(TAG_AGG) << 32) | (aq << 16) | aw);
     }
-    return cr;
 }
 
-// Mode-1 / mode-2 follow-up state of a regime-B bucket.
-struct Defer {
-    uint32_t active, b, cnt;
-    uint32_t nc;         // candidate count (window path) or ~0 = read cand_n
-    uint32_t tail_cand;  // the ragged tail competes in the heap fill
-    float tail_key;
+// ===========================================================================
+// finisher wave
+// ===========================================================================
+__device__ __forceinline__ void release(Ctx &C, uint32_t par, uint32_t j) {
+    Lds &L = C.L;
+    lds_drain();
+    if (flane() == 0) {
+        L.nst[par] = 0;
+        L.nwl[par] = 0;
+        L.qcnt[par] = 0;
+        L.wcnt[par] = 0;
+        L.sdone[par] = 0;
+    }
+    lds_drain();
+    if (flane() == 0) lds_st(&L.fdone, j + 1);
+}
+
+// Prefix counts of chunk c of bucket b: the aggregates of the bucket's chunks
+// before c (tagged 16-byte descriptors, gathered GB per round trip into LDS;
+// stale ones re-polled).  Chunks are taken in order, so these were taken
+// earlier than chunk c and are almost always complete.  The bucket's last
+// chunk thereby also sees every other chunk: its prefix + its own counts are
+// the bucket's totals.
+__device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, uint32_t &P, uint32_t &Wbef) {
+    Lds &L = C.L;
+    const BucketDesc &d = C.A.bk[b];
+    const uint32_t lane = flane();
+    const uint32_t tA = C.tag(TAG_AGG);
+    uint32_t pq = 0, pw = 0;
+    for (uint32_t p0 = 0; p0 < c; p0 += GB) {
+        const uint32_t n = std::min(GB, c - p0);
+        gather16(&C.A.desc[d.cs + p0], n, L.gb);
+        for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            uint64_t a = 0;
+            if (i < n) { const uint4 e = L.gb[i]; a = ((uint64_t)e.y << 32) | e.x; }
+            bool pend = i < n && (uint32_t)(a >> 32) != tA;
+            for (uint32_t spins = 0; __any(pend); ++spins) {
+                __builtin_amdgcn_s_sleep(1);
+                if (pend) {
+                    a = ld_sc1(&C.A.desc[d.cs + p0 + i].agg);
+                    pend = (uint32_t)(a >> 32) != tA;
+                }
+                if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+            }
+            if (i < n) { pq += (uint32_t)(a >> 16) & 0xffffu; pw += (uint32_t)a & 0xffffu; }
+        }
+    }
+    P = uni(wave_sum(pq));
+    Wbef = uni(wave_sum(pw));
+}
+
+// Per-finisher state carried between slots: window lists written but not yet
+// counted (their stores are retired by the next gather), 4 bits per bucket.
+struct FinState {
+    uint64_t pend;
 };
 
-// Distributed rank-and-emit of a collected candidate set: output order is
-// (sum desc, position asc) = ascending composite key (~ord(sum) << 32 | pos);
-// an entry's rank is the number of smaller keys, counted by one wave per
-// entry over the LDS copy of the set (+ the ragged tail when it competes).
-__device__ __forceinline__ void rank_emit(Ctx &C, const BucketDesc &d, const uint64_t *cand, uint32_t cnt,
-                                          uint32_t nc_all, bool add_tail, float tail_key) {
-    Lds &L = C.L;
-    const uint32_t total = nc_all + (add_tail ? 1u : 0u);
-    const uint32_t first_e = C.w * FNW;  // entries handled here: e = w*FNW + wave + k*G*FNW
-    if (first_e >= total) return;
-    const uint32_t tailpos = d.nb * 16;
-    const uint64_t tail_comp = ((uint64_t)(~ford(tail_key)) << 32) | (uint64_t)tailpos;
-    for (uint32_t i = C.ftid(); i < total; i += FWG) L.cand[i] = i < nc_all ? ld_sc1(&cand[i]) : tail_comp;
-    __syncthreads();
-    for (uint32_t e = first_e + C.wave; e < total; e += C.G * FNW) {
-        const uint64_t key = L.cand[e];
-        uint32_t less = 0;
-        for (uint32_t j = C.flane(); j < total; j += 64) less += L.cand[j] < key;
-        const uint32_t rank = wave_sum(less);
-        const bool is_tail = add_tail && key == tail_comp;
-        const bool tail_before = add_tail && tail_comp < key;
-        const uint32_t pos = (uint32_t)key;
-        const uint32_t len = is_tail ? d.tl : 16u;
-        const uint64_t off = (uint64_t)cnt + 16ull * rank - (tail_before ? (uint64_t)(16u - d.tl) : 0ull);
-        if (off < d.dst_len) {
-            const uint32_t Ln = std::min<uint32_t>(len, d.dst_len - (uint32_t)off);
-            if (C.flane() < Ln) {
-                d.val[off + C.flane()] = d.src[(size_t)pos + C.flane()];
-                d.idx[off + C.flane()] = pos + C.flane() + (uint32_t)d.idx_offset;
-            }
-        }
+// Count the pending window lists as in place (the caller drained its stores).
+__device__ __forceinline__ void flush_lists(Ctx &C, FinState &F) {
+    for (uint32_t b = 0; F.pend; ++b, F.pend >>= 4) {
+        const uint32_t n = (uint32_t)(F.pend & 15u);
+        if (n && flane() == 0) atomicAdd(&C.cc()->bk[b].lists, n);
     }
-    __syncthreads();  // L.cand is reused
 }
 
-// ---- finish(b): exchange, regime, emission, AIMD; regime B heap fill ----
+// finish(slot j = chunk k): look-back, ordered emission, window list; the
+// bucket's last chunk also decides the regime, writes tail / AIMD / count and
+// posts the decision for the rankers.
 template <int STAGE>
-__device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &cr, const Prefetch &pf) {
+__device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, FinState &F) {
+    Lds &L = C.L;
+    const uint32_t par = j % NBUF;
+    const uint32_t lane = flane();
+    for (uint32_t spins = 0; lds_ld(&L.sdone[par]) < NS; ++spins) {
+        __builtin_amdgcn_s_sleep(1);
+        if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+    }
+    if (STAGE == 1 || STAGE == 3) {
+        release(C, par, j);
+        return;
+    }
+    const uint32_t b = C.bucket_of(k);
+    const BucketDesc &d = C.A.bk[b];
+    const uint32_t c = k - d.cs;
+    const uint32_t L0 = c * TV16_CHUNK;
+    const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+    const uint32_t qw = uni(L.qcnt[par]);
+    const float t = uni(L.tval[par]), inc = uni(L.incv[par]);
+    if (j < 8) C.stamp(j * 8 + 0, 0);
+
+    // ---- prefix counts of the bucket's earlier chunks ----
+    uint32_t P = 0, Wbef = 0;
+    if (c) {
+        prefix_counts(C, b, c, P, Wbef);
+        flush_lists(C, F);  // the gather retired the earlier chunks' list stores
+    }
+    const uint32_t ww = uni(L.wcnt[par]);
+    if (j < 8) C.stamp(j * 8 + 1, 0);
+
+    // ---- ordered emission of the chunk's qualifying lines with rank < lim ----
+    const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
+    const uint32_t lim = kb + (r ? 1u : 0u);
+    const bool vec = aligned16(d);
+    if (P < lim && qw) {
+        // in-chunk rank from the streaming waves' per-step ballots (bits at 4 * line)
+        const uint32_t nsteps = (nl + 15) / 16;
+        {
+            const uint32_t j0 = 2 * lane, j1 = 2 * lane + 1;
+            const uint32_t c0s = j0 < nsteps ? (uint32_t)__popcll(L.qm[par][j0]) : 0u;
+            const uint32_t c1s = j1 < nsteps ? (uint32_t)__popcll(L.qm[par][j1]) : 0u;
+            const uint32_t ex = wave_incl_scan(c0s + c1s) - (c0s + c1s);
+            L.wt[j0] = ex;
+            L.wt[j1] = ex + c0s;
+        }
+        lds_drain();
+        if (qw <= STAGE_B) {
+            // every qualifying line is staged in LDS: a quad per line
+            const uint32_t q = lane & 3;
+            for (uint32_t e0 = 0; e0 < qw; e0 += 16) {
+                const uint32_t e = e0 + (lane >> 2);
+                if (e >= qw) continue;
+                const uint32_t i = L.stage_line[par][e];
+                const uint32_t jj = i >> 4, ln = (i & 15) * 4;
+                const uint32_t g = P + L.wt[jj] + (uint32_t)__popcll(L.qm[par][jj] & below_mask(ln));
+                if (g >= lim) continue;
+                const uint32_t pos = (L0 + i) * 16 + 4 * q;
+                const uint32_t len = g == kb ? r : 16u;
+                const uint32_t off = 16 * g + 4 * q;
+                const float4 x = L.stage[par][e * 4 + q];
+                const uint32_t bi = pos + (uint32_t)d.idx_offset;
+                if (vec && len == 16) {
+                    *reinterpret_cast<float4 *>(d.val + off) = x;
+                    *reinterpret_cast<uint4 *>(d.idx + off) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                } else {
+                    const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (uint32_t cc = 0; cc < 4; ++cc) {
+                        if (4 * q + cc < len) {
+                            d.val[off + cc] = xs[cc];
+                            d.idx[off + cc] = bi + cc;
+                        }
+                    }
+                }
+            }
+        } else {
+            // staging overflowed (low threshold): the ballots name the lines,
+            // src supplies the data
+            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const uint32_t jj = i >> 4, ln = (i & 15) * 4;
+                const uint64_t m = i < nl ? L.qm[par][jj] : 0ull;
+                if ((m >> ln) & 1ull) {
+                    const uint32_t g = P + L.wt[jj] + (uint32_t)__popcll(m & below_mask(ln));
+                    if (g < lim) emit_line(d, vec, (L0 + i) * 16, 16 * g, g == kb ? r : 16u);
+                }
+            }
+        }
+    }
+
+    // ---- the chunk's window candidates at its exchanged offset (speculative:
+    //      used only if the bucket ends in regime B with the window path) ----
+    if (STAGE != 5 && Wbef + ww + 1 <= CAND_CAP) {
+        // 32-bit window keys (tb-1-u) << 12 | set index, the set in position
+        // order (chunks in order, each list sorted by position), plus the
+        // line positions at [CAND_CAP + index]
+        const uint32_t nwl = uni(lds_ld(&L.nwl[par]));
+        uint32_t *ckey = reinterpret_cast<uint32_t *>(C.cand(b));
+        uint32_t *cpos = ckey + CAND_CAP;
+        const uint32_t tb = f2u(t);
+        if (nwl <= WL_B) {
+            const uint64_t e = lane < nwl ? L.wl[par][lane] : ~0ull;
+            const uint32_t mypos = (uint32_t)e;
+            uint32_t before = 0;
+            for (uint32_t l = 0; l < nwl; ++l) before += (uint32_t)L.wl[par][l] < mypos;
+            if (lane < nwl) {
+                const uint32_t u = ~(uint32_t)(e >> 32) & 0x7fffffffu;
+                const uint32_t idx = Wbef + before;
+                st_sc1(&ckey[idx], ((tb - 1u - u) << 12) | idx);
+                st_sc1(&cpos[idx], mypos);
+            }
+        } else {  // the LDS list overflowed: list the window from src, in order
+            const uint32_t wlo = tb > WIN ? tb - WIN : 0u;
+            uint32_t base = Wbef;
+            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const uint32_t u = i < nl ? f2u(lane_line_sum(d.src + (size_t)(L0 + i) * 16)) : 0xffffffffu;
+                const bool p = u >= wlo && u < tb;
+                const uint64_t m = __ballot(p);
+                if (p) {
+                    const uint32_t idx = base + (uint32_t)__popcll(m & below_mask(lane));
+                    st_sc1(&ckey[idx], ((tb - 1u - u) << 12) | idx);
+                    st_sc1(&cpos[idx], (L0 + i) * 16);
+                }
+                base += (uint32_t)__popcll(m);
+            }
+        }
+    }
+    if (((F.pend >> (4 * b)) & 15u) == 15u) {  // counter full: retire and count now
+        vm_drain();
+        flush_lists(C, F);
+    }
+    F.pend += 1ull << (4 * b);
+    release(C, par, j);
+    if (j < 8) C.stamp(j * 8 + 2, 0);
+
+    // ---- the bucket's last chunk: regime, tail, AIMD, count, decision ----
+    if (c + 1 == d.nc) {
+        const uint32_t Qtot = P + qw, Wtot = Wbef + ww;
+        const uint32_t c0 = Qtot >= lim ? d.dst_len : 16u * Qtot;
+        bool tail_cand = false;
+        float tail_key = 0.f;
+        uint32_t ct = 0;
+        if (c0 < d.dst_len && d.tl) {  // stage 3: the ragged tail's signed, sequential sum
+            const float *tp = d.src + (size_t)d.nb * 16;
+            float s = 0.f;
+            for (uint32_t i = 0; i < d.tl; ++i) s += tp[i];
+            s = uni(s);
+            if (s * 16.0f >= t * (float)d.tl) ct = std::min(d.dst_len - c0, d.tl);
+            else { tail_cand = true; tail_key = s * 16.0f / (float)d.tl; }
+        }
+        const uint32_t cnt = c0 + ct;
+        const bool regimeB = cnt < d.dst_len;
+        if (lane == 0) {
+            if (ct) {
+                const size_t p0 = (size_t)d.nb * 16;
+                for (uint32_t i = 0; i < ct; ++i) {
+                    d.val[c0 + i] = d.src[p0 + i];
+                    d.idx[c0 + i] = (uint32_t)(p0 + i) + (uint32_t)d.idx_offset;
+                }
+            }
+            d.state->t = regimeB ? (float)((double)t * 0.99) : t + inc;
+            d.state->inc = inc;
+            d.state->init = 1;
+            *d.count_out = (uint32_t)std::min<uint64_t>(d.dst_len, (uint64_t)d.nb * 16 + d.tl);
+        }
+        const uint32_t ncand = d.nb - Qtot;  // non-qualifying full lines
+        const uint32_t M = regimeB ? std::min((d.dst_len - cnt + 15u) / 16u, ncand) : 0u;
+        uint32_t flags = 0;
+        if (regimeB && STAGE != 5) {
+            flags = DEC_B | (tail_cand ? DEC_TAIL : 0u) | (M > 0 && Wtot >= M && Wtot + 1 <= CAND_CAP ? DEC_WIN : 0u);
+        }
+        Decision &D = C.ctl()->dec[b];
+        if (lane == 0) {
+            st_sc1(&D.w[1], ((uint64_t)cnt << 32) | M);
+            st_sc1(&D.w[2], ((uint64_t)Wtot << 32) | __float_as_uint(tail_key));
+            st_sc1(&D.w[3], ((uint64_t)Qtot << 32) | __float_as_uint(t));
+        }
+        vm_drain();
+        if (lane == 0) st_sc1(&D.w[0], ((uint64_t)C.tag(TAG_DEC) << 32) | flags);
+    }
+}
+
+// ===========================================================================
+// ranker wave: the regime-B heap fill, top candidates by (sum desc, pos asc)
+// ===========================================================================
+// Rank-and-emit of a collected candidate set: output order is ascending
+// composite key; an entry's rank is the number of smaller keys.  Ranker r of
+// the R taking part ranks entries r, r + R, ... (8 at a time) in one pass over
+// an LDS copy of the set (+ the ragged tail when it competes).
+__device__ __forceinline__ void rank_emit(Ctx &C, uint32_t r, uint32_t R, const BucketDesc &d, const uint64_t *cand,
+                                          uint32_t cnt, uint32_t nc_all, bool add_tail, float tail_key) {
+    Lds &L = C.L;
+    const uint32_t total = nc_all + (add_tail ? 1u : 0u);
+    if (r >= total) return;
+    const uint32_t lane = flane();
+    const uint32_t tailpos = d.nb * 16;
+    const uint64_t tail_comp = ((uint64_t)(~ford(tail_key)) << 32) | (uint64_t)tailpos;
+    if (nc_all) gather16(cand, (nc_all + 1) / 2, L.cand);
+    if (add_tail && lane == 0) L.cand[nc_all] = tail_comp;
+    lds_drain();
+    constexpr uint32_t KB = 8;
+    const uint32_t ne = (total - r + R - 1) / R;
+    for (uint32_t k0 = 0; k0 < ne; k0 += KB) {
+        uint64_t key[KB];
+        uint32_t less[KB];
+#pragma unroll
+        for (uint32_t k = 0; k < KB; ++k) {
+            const uint32_t e = r + (k0 + k) * R;
+            key[k] = k0 + k < ne ? L.cand[e] : 0ull;
+            key[k] = ((uint64_t)uni((uint32_t)(key[k] >> 32)) << 32) | uni((uint32_t)key[k]);
+            less[k] = 0;
+        }
+        for (uint32_t jj = lane; jj < total; jj += 64) {
+            const uint64_t x = L.cand[jj];
+#pragma unroll
+            for (uint32_t k = 0; k < KB; ++k) less[k] += x < key[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KB; ++k) {
+            if (k0 + k >= ne) break;
+            const uint32_t rank = wave_sum(less[k]);
+            const bool is_tail = add_tail && key[k] == tail_comp;
+            const bool tail_before = add_tail && tail_comp < key[k];
+            const uint32_t pos = (uint32_t)key[k];
+            const uint32_t len = is_tail ? d.tl : 16u;
+            const uint64_t off = (uint64_t)cnt + 16ull * rank - (tail_before ? (uint64_t)(16u - d.tl) : 0ull);
+            if (off < d.dst_len) {
+                const uint32_t Ln = std::min<uint32_t>(len, d.dst_len - (uint32_t)off);
+                if (lane < Ln) {
+                    d.val[off + lane] = d.src[(size_t)pos + lane];
+                    d.idx[off + lane] = pos + lane + (uint32_t)d.idx_offset;
+                }
+            }
+        }
+    }
+}
+
+// Window path rank-and-emit.  The set holds Wtot unique 32-bit keys
+// (tb-1-u) << 12 | index, ascending = (sum desc, position asc), index in
+// position order.  Each ranker gathers it into LDS, counting-sorts it by the
+// top 10 bits (LDS atomics), and ranks its entries r, r + R, ... as bin start
+// + the smaller keys of the same bin (a few); the ragged tail competes as
+// index Wtot when its key falls inside the window.
+__device__ __forceinline__ void rank_window(Ctx &C, uint32_t r, uint32_t R, const BucketDesc &d, uint32_t b,
+                                            uint32_t cnt, uint32_t Wtot, bool tail, float tail_key, uint32_t tb) {
+    Lds &L = C.L;
+    const uint32_t lane = flane();
+    const uint32_t *ckey = reinterpret_cast<const uint32_t *>(C.cand(b));
+    const uint32_t *cpos = ckey + CAND_CAP;
+    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;
+    const uint32_t ut = f2u(tail_key);  // a negative tail key has the sign bit: never in the window
+    const bool tail_in = tail && ut >= wlo && ut < tb && Wtot < CAND_CAP;
+    const uint32_t tail_k = ((tb - 1u - ut) << 12) | Wtot;
+    if (Wtot) gather16(ckey, (Wtot + 3) / 4, L.wr.key);
+    const uint32_t total = Wtot + (tail_in ? 1u : 0u);
+    if (tail_in && lane == 0) L.wr.key[Wtot] = tail_k;
+    for (uint32_t i = lane; i < WBINS; i += 64) L.wr.bin[i] = 0;
+    lds_drain();
+    constexpr uint32_t SH = 29 - 10;  // keys < 2^29
+    for (uint32_t i = lane; i < total; i += 64) atomicAdd(&L.wr.bin[L.wr.key[i] >> SH], 1u);
+    lds_drain();
+    {  // exclusive scan of the bins, 16 per lane (read twice: no register array)
+        constexpr uint32_t BPL = WBINS / 64;
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < BPL; ++q) sum += L.wr.bin[lane * BPL + q];
+        uint32_t run = wave_incl_scan(sum) - sum;
+        for (uint32_t q = 0; q < BPL; ++q) {
+            const uint32_t c = L.wr.bin[lane * BPL + q];
+            L.wr.bin[lane * BPL + q] = run;
+            run += c;
+        }
+    }
+    lds_drain();
+    for (uint32_t i = lane; i < total; i += 64) {
+        const uint32_t k = L.wr.key[i];
+        L.wr.srt[atomicAdd(&L.wr.bin[k >> SH], 1u)] = k;  // bin[x] ends as the end of bin x
+    }
+    lds_drain();
+    const uint32_t ne = (total - r + R - 1) / R;
+    const bool vec = aligned16(d);
+    const uint32_t tailpos = d.nb * 16;
+    for (uint32_t e0 = 0; e0 < ne; e0 += 64) {
+        // one entry per lane: its rank, position, length and output offset
+        const uint32_t q = e0 + lane;
+        if (q < ne) {
+            const uint32_t k = L.wr.key[r + q * R];
+            const uint32_t bn = k >> SH;
+            const uint32_t lo = bn ? L.wr.bin[bn - 1] : 0u, hi = L.wr.bin[bn];
+            uint32_t rank = lo;
+            for (uint32_t x = lo; x < hi; ++x) rank += L.wr.srt[x] < k;
+            const uint32_t idx = k & 0xfffu;
+            const bool is_tail = tail_in && idx == Wtot;
+            const bool tail_before = tail_in && tail_k < k;
+            const uint64_t off = (uint64_t)cnt + 16ull * rank - (tail_before ? (uint64_t)(16u - d.tl) : 0ull);
+            const uint32_t pos = is_tail ? tailpos : ld_sc1(&cpos[idx]);
+            const uint32_t len = off < d.dst_len ? std::min<uint32_t>(is_tail ? d.tl : 16u, d.dst_len - (uint32_t)off) : 0u;
+            L.wr.ent[lane] = make_uint4(rank, pos, len, (uint32_t)std::min<uint64_t>(off, 0xffffffffu));
+        }
+        lds_drain();
+        // emission: a quad of lanes per entry, two groups of 16 entries in
+        // flight (their loads issued before their stores)
+        const uint32_t nq = std::min(64u, ne - e0);
+        const uint32_t c4 = 4 * (lane & 3);
+        for (uint32_t g0 = 0; g0 < 4; g0 += 2) {
+            float4 x[2];
+            uint4 en[2];
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t el = (g0 + h) * 16 + (lane >> 2);
+                en[h] = el < nq ? L.wr.ent[el] : make_uint4(0, 0, 0, 0);
+                x[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (en[h].z == 16 && vec) x[h] = *reinterpret_cast<const float4 *>(d.src + (size_t)en[h].y + c4);
+            }
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t len = en[h].z, pos = en[h].y, off = en[h].w;
+                if (!len) continue;
+                const uint32_t bi = pos + c4 + (uint32_t)d.idx_offset;
+                if (len == 16 && vec) {
+                    *reinterpret_cast<float4 *>(d.val + off + c4) = x[h];
+                    *reinterpret_cast<uint4 *>(d.idx + off + c4) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                } else {
+                    for (uint32_t cc = 0; cc < 4; ++cc) {
+                        if (c4 + cc < len) {
+                            d.val[off + c4 + cc] = d.src[(size_t)pos + c4 + cc];
+                            d.idx[off + c4 + cc] = bi + cc;
+                        }
+                    }
+                }
+            }
+        }
+        lds_drain();
+    }
+}
+
+// Rare paths: the window does not hold the top M -> radix descent over the
+// bucket's line sums (ranker w takes chunks w, w + G, ...; sums recomputed
+// from src into sums_g) with grid barriers among the rankers, then rank and emit.
+__device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, uint32_t cnt, uint32_t M, float t,
+                                          float tail_key) {
     const BucketDesc &d = C.A.bk[b];
     Lds &L = C.L;
-    FillCtl *ctl = C.ctl();
-    const uint32_t par = b % NBUF;
-    const uint32_t G = C.G, w = C.w, tid = C.ftid(), lane = C.flane(), wave = C.wave;
-    const uint32_t L0 = C.range_lo(d), nl = C.range_len(d);
-    const bool lds_sums = nl <= LINES_B;
-    const bool vec = ((reinterpret_cast<uintptr_t>(d.src) | reinterpret_cast<uintptr_t>(d.idx) |
-                       reinterpret_cast<uintptr_t>(d.val)) & 15u) == 0;
-    auto get_sum = [&](uint32_t i) -> float { return lds_sums ? L.sum[par][i] : d.sums_g[L0 + i]; };
-    const float t = cr.t, inc = cr.inc;
+    const uint32_t G = C.G, w = C.w, lane = flane();
+    const bool vec = aligned16(d);
     const uint32_t tb = f2u(t);
-    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;
-    const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
-    auto bc = [&]() { return &C.ctl()->cc[C.A.epoch & 1u].bk[b]; };  // per use: not held live
-    uint64_t *cand = C.cand() + (size_t)(b & 3u) * CAND_CAP;
-
-    C.sub(1);
-    // ---- count exchange: wave j gathers workgroups [64j, 64j+64) (one
-    //      granule pair per lane, all in flight), re-polling only stale ones ----
-    const uint32_t nsw = (G + 63) / 64;
-    if (wave < nsw) {
-        const uint32_t tg = C.tag(b);
-        const uint32_t v = wave * 64 + lane;
-        const uint4 e = L.pf[v];  // prefetched during this bucket's successor's scan
-        uint64_t g = ((uint64_t)e.y << 32) | e.x, g2 = ((uint64_t)e.w << 32) | e.z;
-        bool pend = v < G && ((uint32_t)(g >> 32) != tg || (uint32_t)(g2 >> 32) != tg);
-        if (C.probe && lane == 0) atomicAdd(&L.stamp[16 + 8], (uint32_t)__popcll(__ballot(pend)));
-        uint32_t polls = 0;
-        for (uint32_t spins = 0;; ++spins) {
-            if (!__any(pend)) break;
-            ++polls;
-            if (pend) {
-                g = ld_sc1(&ctl->gran[b][v][0]);
-                g2 = ld_sc1(&ctl->gran[b][v][1]);
-                pend = (uint32_t)(g >> 32) != tg || (uint32_t)(g2 >> 32) != tg;
-            }
-            if (!__any(pend)) break;
-            __builtin_amdgcn_s_sleep(1);
-            if (spins > (1u << 22)) { atomicOr(C.fail(), (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+    const bool tail_cand = (flags & DEC_TAIL) != 0;
+    uint64_t *cand = C.cand(b);
+    BucketCtl *bc = &C.cc()->bk[b];
+    // this ranker's lines: chunks c = w, w + G, ... of the bucket
+    auto for_lines = [&](auto &&fn) {
+        for (uint32_t c = w; c < d.nc; c += G) {
+            const uint32_t L0 = c * TV16_CHUNK;
+            const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+            for (uint32_t i0 = 0; i0 < nl; i0 += 64) fn(L0 + i0 + lane, L0 + i0 + lane < L0 + nl, c);
         }
-        if (C.probe && lane == 0) atomicMax(&L.stamp[16 + 9], polls);
-        const uint32_t c = v < G ? (uint32_t)g : 0u, cw = v < G ? (uint32_t)g2 : 0u;
-        const uint32_t tot = wave_sum(c), wtot = wave_sum(cw);
-        const uint32_t bef = wave_sum(v < w ? c : 0u), wbef = wave_sum(v < w ? cw : 0u);
-        if (lane == 0) {
-            L.xch[wave][0] = bef;
-            L.xch[wave][1] = tot;
-            L.xch[wave][2] = wbef;
-            L.xch[wave][3] = wtot;
-        }
-    }
-    __syncthreads();
-    uint32_t P = 0, Qtot = 0, Wbef = 0, Wtot = 0;
-    for (uint32_t j = 0; j < nsw; ++j) {
-        P += L.xch[j][0];
-        Qtot += L.xch[j][1];
-        Wbef += L.xch[j][2];
-        Wtot += L.xch[j][3];
-    }
-    P = uni(P);
-    Qtot = uni(Qtot);
-    Wbef = uni(Wbef);
-    Wtot = uni(Wtot);
-    __syncthreads();
-    if (STAGE == 2) return Defer{};
-
-    C.sub(2);
-    // ---- regime (identical in every workgroup) ----
-    const uint32_t lim = kb + (r ? 1u : 0u);
-    const uint32_t c0 = Qtot >= lim ? d.dst_len : 16u * Qtot;
-    bool tail_cand = false;
-    float tail_key = 0.f;
-    uint32_t ct = 0;
-    if (c0 < d.dst_len && d.tl) {
-        const float *tp = d.src + (size_t)d.nb * 16;
-        float s = 0.f;
-        for (uint32_t i = 0; i < d.tl; ++i) s += tp[i];
-        s = uni(s);
-        if (s * 16.0f >= t * (float)d.tl) ct = std::min(d.dst_len - c0, d.tl);
-        else { tail_cand = true; tail_key = s * 16.0f / (float)d.tl; }
-    }
-    const uint32_t cnt = c0 + ct;
-    const bool regimeB = cnt < d.dst_len;
-
-    // ---- ordered emission of this range's qualifying lines ----
-    // In-range rank of line i = j*FWG + tid via ballot masks (order j, wave, lane).
-    if (P < lim && cr.qw) {
-        const uint32_t nj = (nl + FWG - 1) / FWG;
-        if (nj <= MAX_J && cr.qw <= STAGE_B) {
-            // every qualifying line is staged in LDS: one thread per staged line
-            for (uint32_t j = 0; j < nj; ++j) {
-                const uint32_t i = j * FWG + tid;
-                const uint64_t bal = __ballot(i < nl && get_sum(i) >= t);
-                if (lane == 0) { L.mask[j * FNW + wave] = bal; L.wt[j * FNW + wave] = (uint32_t)__popcll(bal); }
-            }
-            __syncthreads();
-            if (tid == 0) {
-                uint32_t acc = 0;
-                for (uint32_t i = 0; i < nj * FNW; ++i) { const uint32_t x = L.wt[i]; L.wt[i] = acc; acc += x; }
-            }
-            __syncthreads();
-            for (uint32_t e = tid; e < cr.qw; e += FWG) {
-                const uint32_t i = L.stage_line[par][e];
-                const uint32_t grp = (i / FWG) * FNW + ((i % FWG) >> 6), ln = i & 63;
-                const uint64_t m = L.mask[grp];
-                const uint32_t g = P + L.wt[grp] + (uint32_t)__popcll(m & (ln ? (~0ull >> (64 - ln)) : 0ull));
-                if (g < lim) {
-                    const uint32_t pos = (L0 + i) * 16;
-                    const uint32_t len = g == kb ? r : 16u;
-                    const uint32_t off = 16 * g;
-                    if (vec && len == 16) {
-                        float4 *v4 = reinterpret_cast<float4 *>(d.val + off);
-                        uint4 *i4 = reinterpret_cast<uint4 *>(d.idx + off);
-                        const uint32_t bi = pos + (uint32_t)d.idx_offset;
-#pragma unroll
-                        for (uint32_t c = 0; c < 4; ++c) {
-                            v4[c] = L.stage[par][e * 4 + c];
-                            i4[c] = make_uint4(bi + 4 * c, bi + 4 * c + 1, bi + 4 * c + 2, bi + 4 * c + 3);
-                        }
-                    } else {
-                        const float *sv = reinterpret_cast<const float *>(&L.stage[par][e * 4]);
-                        for (uint32_t c = 0; c < len; ++c) {
-                            d.val[off + c] = sv[c];
-                            d.idx[off + c] = pos + c + (uint32_t)d.idx_offset;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-        } else {
-            // staging overflowed (low threshold) or a long range: re-read src
-            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-            uint32_t base = P;
-            for (uint32_t j0 = 0; j0 < nj && base < lim; j0 += MAX_J) {
-                const uint32_t jn = std::min(nj - j0, MAX_J);
-                uint32_t flags = 0;
-                for (uint32_t j = 0; j < jn; ++j) {
-                    const uint32_t i = (j0 + j) * FWG + tid;
-                    const bool f = i < nl && get_sum(i) >= t;
-                    flags |= (uint32_t)f << j;
-                    const uint64_t bal = __ballot(f);
-                    if (lane == 0) L.wt[j * FNW + wave] = (uint32_t)__popcll(bal);
-                }
-                __syncthreads();
-                if (tid == 0) {
-                    uint32_t acc = 0;
-                    for (uint32_t i = 0; i < jn * FNW; ++i) { const uint32_t x = L.wt[i]; L.wt[i] = acc; acc += x; }
-                    L.wt[MAX_J * FNW] = acc;
-                }
-                __syncthreads();
-                for (uint32_t j = 0; j < jn; ++j) {
-                    const uint64_t bal = __ballot((flags >> j) & 1u);
-                    if ((flags >> j) & 1u) {
-                        const uint32_t g = base + L.wt[j * FNW + wave] + (uint32_t)__popcll(bal & lt);
-                        if (g < lim) {
-                            const uint32_t line = L0 + (j0 + j) * FWG + tid;
-                            emit_line(d, vec, line * 16, 16 * g, g == kb ? r : 16u);
-                        }
-                    }
-                }
-                base += L.wt[MAX_J * FNW];
-                __syncthreads();
-            }
-        }
-    }
-
-    C.sub(3);
-    // ---- tail, AIMD, count (workgroup 0) ----
-    if (w == 0 && tid == 0) {
-        if (ct) {
-            const size_t p0 = (size_t)d.nb * 16;
-            for (uint32_t i = 0; i < ct; ++i) {
-                d.val[c0 + i] = d.src[p0 + i];
-                d.idx[c0 + i] = (uint32_t)(p0 + i) + (uint32_t)d.idx_offset;
-            }
-        }
-        d.state->t = regimeB ? (float)((double)t * 0.99) : t + inc;
-        d.state->inc = inc;
-        d.state->init = 1;
-        *d.count_out = (uint32_t)std::min<uint64_t>(d.dst_len, (uint64_t)d.nb * 16 + d.tl);
-    }
-    C.sub(4);
-    if (!regimeB || STAGE == 5) return Defer{};
-
-    // ---- heap fill = top candidates by (sum desc, position asc) ----
-    const uint32_t rem = d.dst_len - cnt;
-    const uint32_t ncand = d.nb - Qtot;  // non-qualifying full lines
-    const uint32_t M = std::min((rem + 15u) / 16u, ncand);
-    const uint32_t hi0 = tb - 1u;        // largest candidate key (keys u < tb)
-
-    // mode 1: collect keys >= blo; mode 2: ties at ustar taken in position order
+    };
+    for_lines([&](uint32_t li, bool ok, uint32_t) {
+        if (ok) d.sums_g[li] = lane_line_sum(d.src + (size_t)li * 16);
+    });
+    vm_drain();
+    auto get_sum = [&](uint32_t li) -> float { return d.sums_g[li]; };
+    const uint32_t hi0 = tb - 1u;  // largest candidate key (keys u < tb)
     uint32_t mode = 1, blo = tb, ustar = 0, greater = 0;
-    const bool win_ok = M > 0 && Wtot >= M && Wtot + 1 <= CAND_CAP;
-    if (win_ok) {
-        blo = wlo;  // the window holds the top M: no histogram needed
-    } else if (M > 0) {
-        for (uint32_t i = tid; i < HBINS; i += FWG) L.hist[i] = 0;
-        __syncthreads();
-        for (uint32_t i = tid; i < nl; i += FWG) {
-            const uint32_t u = f2u(get_sum(i));
+    if (M > 0) {
+        for (uint32_t i = lane; i < HBINS; i += 64) L.hist[i] = 0;
+        lds_drain();
+        for_lines([&](uint32_t li, bool ok, uint32_t) {
+            if (!ok) return;
+            const uint32_t u = f2u(get_sum(li));
             if (u < tb) atomicAdd(&L.hist[std::min((hi0 - u) >> L1_SHIFT, HBINS - 1)], 1u);
+        });
+        lds_drain();
+        for (uint32_t i = lane; i < HBINS; i += 64) {
+            const uint32_t h = L.hist[i];
+            if (h) atomicAdd(&bc->hist[0][i], h);
         }
-        __syncthreads();
-        for (uint32_t i = tid; i < HBINS; i += FWG)
-            if (L.hist[i]) atomicAdd(&bc()->hist[0][i], L.hist[i]);
         C.grid_sync();
         uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
         bool ovf = true;
+        constexpr uint32_t BPL = HBINS / 64;  // bins per lane
         for (;;) {
             // locate the bin holding rank `need` (1-based) counting down from hi
             const uint32_t need = M - above;
-            const uint32_t cbin = tid < HBINS ? ld_acq_relaxed(&bc()->hist[lvl][tid]) : 0u;
-            uint32_t total;
-            const uint32_t before = blk_excl_scan<FNW>(cbin, L.sh, &total);
-            if (tid == 0) { L.dec[2] = 0xffffffffu; L.dec[3] = 0; L.dec[4] = 0; }
-            __syncthreads();
-            if (tid < HBINS && need > before && need <= before + cbin) { L.dec[2] = tid; L.dec[3] = before; L.dec[4] = cbin; }
-            __syncthreads();
-            const uint32_t bstar = uni(L.dec[2]), cum = uni(L.dec[3]), hb = uni(L.dec[4]);
-            __syncthreads();
+            uint32_t loc = 0;
+            for (uint32_t jj = 0; jj < BPL; ++jj) loc += ld_acq_relaxed(&bc->hist[lvl][lane * BPL + jj]);
+            const uint32_t incl = wave_incl_scan(loc);
+            const uint32_t excl = incl - loc;
+            const uint64_t fm = __ballot(need > excl && need <= incl);
+            uint32_t bstar = 0xffffffffu, cum = 0, hb = 0;
+            if (fm) {
+                const uint32_t src_lane = (uint32_t)__ffsll((long long)fm) - 1u;
+                if (lane == src_lane) {
+                    uint32_t cc = excl;
+                    for (uint32_t jj = 0; jj < BPL; ++jj) {
+                        const uint32_t h = ld_acq_relaxed(&bc->hist[lvl][lane * BPL + jj]);
+                        if (need <= cc + h) { bstar = lane * BPL + jj; cum = cc; hb = h; break; }
+                        cc += h;
+                    }
+                }
+                bstar = (uint32_t)__builtin_amdgcn_readlane((int)bstar, (int)src_lane);
+                cum = (uint32_t)__builtin_amdgcn_readlane((int)cum, (int)src_lane);
+                hb = (uint32_t)__builtin_amdgcn_readlane((int)hb, (int)src_lane);
+            }
             if (bstar == 0xffffffffu) {  // histogram does not reach `need`: collect all
-                if (tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_LEVELS);
+                if (lane == 0) C.fail(FAIL_LEVELS);
                 mode = 1; blo = 0;
                 break;
             }
@@ -641,7 +918,7 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
                 above += cum;
                 const uint64_t width = (uint64_t)(HBINS - 1) << s;
                 if ((uint64_t)hi < width) {
-                    if (tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_LEVELS);
+                    if (lane == 0) C.fail(FAIL_LEVELS);
                     mode = 1; blo = 0;
                     break;
                 }
@@ -662,209 +939,239 @@ __device__ __forceinline__ Defer finish_bucket(Ctx &C, uint32_t b, const Carry &
                 s = s >= 10 ? s - 10 : 0;
             }
             if (++lvl >= MAX_LEVELS) {
-                if (tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_LEVELS);
+                if (lane == 0) C.fail(FAIL_LEVELS);
                 mode = 1; blo = lo;
                 break;
             }
-            for (uint32_t i = tid; i < HBINS; i += FWG) L.hist[i] = 0;
-            __syncthreads();
-            for (uint32_t i = tid; i < nl; i += FWG) {
-                const uint32_t u = f2u(get_sum(i));
+            for (uint32_t i = lane; i < HBINS; i += 64) L.hist[i] = 0;
+            lds_drain();
+            for_lines([&](uint32_t li, bool ok, uint32_t) {
+                if (!ok) return;
+                const uint32_t u = f2u(get_sum(li));
                 if (u < tb && u >= lo && u <= hi) atomicAdd(&L.hist[(hi - u) >> s], 1u);
+            });
+            lds_drain();
+            for (uint32_t i = lane; i < HBINS; i += 64) {
+                const uint32_t h = L.hist[i];
+                if (h) atomicAdd(&bc->hist[lvl][i], h);
             }
-            __syncthreads();
-            for (uint32_t i = tid; i < HBINS; i += FWG)
-                if (L.hist[i]) atomicAdd(&bc()->hist[lvl][i], L.hist[i]);
             C.grid_sync();
         }
     }
 
     const uint32_t tailpos = d.nb * 16;
     const bool tail_in_greater = tail_cand && mode == 2 && tail_key > u2f(ustar);
-    // collect (write-through): mode 1 -> keys in [blo, tb); mode 2 -> keys in (ustar, tb).
-    // The window path knows every workgroup's slot range from the exchanged
-    // window counts (no atomics); the rare histogram paths append with one
-    // atomic per workgroup and step.
+    // collect: mode 1 -> keys in [blo, tb); mode 2 -> keys in (ustar, tb);
+    // one slot range per ranker; mode 2 also counts each chunk's ties at ustar
     if (M > 0) {
         const uint32_t kmin = mode == 1 ? blo : ustar + 1;
-        uint32_t mine = 0, run = Wbef;
-        for (uint32_t i0 = 0; i0 < nl; i0 += FWG) {
-            const uint32_t i = i0 + tid;
-            uint32_t u = 0;
-            bool p = false;
-            if (i < nl) {
-                u = f2u(get_sum(i));
-                p = u < tb && u >= kmin;
-                mine += mode == 2 && u == ustar;
+        uint32_t mine = 0;
+        for_lines([&](uint32_t li, bool ok, uint32_t) {
+            if (!ok) return;
+            const uint32_t u = f2u(get_sum(li));
+            mine += u < tb && u >= kmin;
+        });
+        mine = uni(wave_sum(mine));
+        uint32_t o = 0;
+        if (lane == 0 && mine) o = atomicAdd(&bc->cand_n, mine);
+        uint32_t base = uni(o);
+        for (uint32_t c = w; c < d.nc; c += G) {
+            const uint32_t L0 = c * TV16_CHUNK;
+            const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+            uint32_t ties = 0;
+            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                uint32_t u = 0;
+                bool p = false;
+                if (i < nl) {
+                    u = f2u(get_sum(L0 + i));
+                    p = u < tb && u >= kmin;
+                    ties += mode == 2 && u == ustar;
+                }
+                const uint64_t m = __ballot(p);
+                const uint32_t ex = (uint32_t)__popcll(m & below_mask(lane));
+                if (p && base + ex < CAND_CAP) st_sc1(&cand[base + ex], cand_key(u, (L0 + i) * 16));
+                base += (uint32_t)__popcll(m);
             }
-            uint32_t n_here;
-            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, L.sh, &n_here);
-            if (!n_here) continue;
-            uint32_t base;
-            if (win_ok) {
-                base = run;
-                run += n_here;
-            } else {
-                if (tid == 0) L.dec[7] = atomicAdd(&bc()->cand_n, n_here);
-                __syncthreads();
-                base = L.dec[7];
-                __syncthreads();
+            if (mode == 2) {
+                const uint32_t ct = uni(wave_sum(ties));
+                if (lane == 0) st_sc1(&C.A.desc[d.cs + c].ties, ((uint64_t)C.tag(TAG_TIE) << 32) | ct);
             }
-            if (p && base + ex < CAND_CAP)
-                st_sc1(&cand[base + ex], ((uint64_t)(~(u | 0x80000000u)) << 32) | (uint64_t)((L0 + i) * 16));
         }
-        if (mode == 2) {
-            const uint32_t my_ties = (uint32_t)blk_sum64<FNW>(mine, L.sh64);
-            if (tid == 0) st_sc1(&ctl->wg_ties[b & 3u][w], my_ties);
-        }
-    }
-    C.sub(5);
-    if (mode == 1) {
-        // The common case: publish "candidates written" and rank the set
-        // after the next bucket's scan (rank_deferred), when every workgroup's
-        // candidates are long in place -- no grid barrier on the critical path.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) st_sc1(&ctl->cdone[b][w], (uint64_t)C.tag(b) << 32);
-        Defer D;
-        D.active = 1;
-        D.b = b;
-        D.cnt = cnt;
-        D.nc = win_ok ? Wtot : 0xffffffffu;
-        D.tail_cand = tail_cand ? 1u : 0u;
-        D.tail_key = tail_key;
-        return D;
     }
     C.grid_sync();  // every append / tie count is visible
-    {  // mode 2: lines tied at ustar, in position order after the greater keys
-        uint64_t pb = 0, pt = 0;
-        for (uint32_t i = tid; i < G; i += FWG) {
-            const uint32_t x = ld_acq_relaxed(&ctl->wg_ties[b & 3u][i]);
-            pt += x;
-            if (i < w) pb += x;
-        }
-        uint32_t rank = (uint32_t)blk_sum64<FNW>(pb, L.sh64);
-        const uint32_t all_ties = (uint32_t)blk_sum64<FNW>(pt, L.sh64);
+    if (mode == 2) {  // lines tied at ustar, in position order after the greater keys
         const uint32_t base = cnt + 16u * greater + (tail_in_greater ? d.tl : 0u);
-        for (uint32_t i0 = 0; i0 < nl; i0 += FWG) {
-            const uint32_t i = i0 + tid;
-            const bool p = i < nl && f2u(get_sum(i)) == ustar;
-            uint32_t n_here;
-            const uint32_t ex = blk_excl_scan<FNW>((uint32_t)p, L.sh, &n_here);
-            if (p) {
-                const uint64_t off = (uint64_t)base + 16ull * (rank + ex);
-                if (off < d.dst_len)
-                    emit_line(d, vec, (L0 + i) * 16, (uint32_t)off, std::min<uint32_t>(16u, d.dst_len - (uint32_t)off));
+        uint32_t all_ties = 0;
+        for (uint32_t c = lane; c < d.nc; c += 64) all_ties += (uint32_t)ld_sc1(&C.A.desc[d.cs + c].ties);
+        all_ties = uni(wave_sum(all_ties));
+        for (uint32_t c = w; c < d.nc; c += G) {
+            uint32_t before = 0;
+            for (uint32_t c2 = lane; c2 < c; c2 += 64) before += (uint32_t)ld_sc1(&C.A.desc[d.cs + c2].ties);
+            uint32_t rank = uni(wave_sum(before));
+            const uint32_t L0 = c * TV16_CHUNK;
+            const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const bool p = i < nl && f2u(get_sum(L0 + i)) == ustar;
+                const uint64_t m = __ballot(p);
+                if (p) {
+                    const uint32_t ex = (uint32_t)__popcll(m & below_mask(lane));
+                    const uint64_t off = (uint64_t)base + 16ull * (rank + ex);
+                    if (off < d.dst_len)
+                        emit_line(d, vec, (L0 + i) * 16, (uint32_t)off,
+                                  std::min<uint32_t>(16u, d.dst_len - (uint32_t)off));
+                }
+                rank += (uint32_t)__popcll(m);
             }
-            rank += n_here;
         }
-        if (w == 0 && tid == 0 && tail_cand && tail_key == u2f(ustar)) {
+        if (w == 0 && lane == 0 && tail_cand && tail_key == u2f(ustar)) {
             const uint64_t off = (uint64_t)base + 16ull * all_ties;
             if (off < d.dst_len)
                 emit_line(d, false, tailpos, (uint32_t)off, std::min<uint32_t>(d.tl, d.dst_len - (uint32_t)off));
         }
     }
-    uint32_t nc_all = uni(ld_acq_relaxed(&bc()->cand_n));
+    uint32_t nc_all = uni(ld_acq_relaxed(&bc->cand_n));
     if (nc_all > CAND_CAP) {
-        if (w == 0 && tid == 0) atomicOr(C.fail(), (uint32_t)FAIL_CAND_OVERFLOW);
+        if (w == 0 && lane == 0) C.fail(FAIL_CAND_OVERFLOW);
         nc_all = CAND_CAP;
     }
-    rank_emit(C, d, cand, cnt, nc_all, tail_in_greater && nc_all < CAND_CAP, tail_key);
-    return Defer{};
+    const bool add_tail = mode == 1 ? tail_cand : tail_in_greater;
+    rank_emit(C, C.w, C.G, d, cand, cnt, nc_all, add_tail && nc_all < CAND_CAP, tail_key);
 }
 
-// Deferred rank-and-emit of a mode-1 candidate set (bucket D.b), run one
-// bucket later.  Workgroups with no entries to rank return at once when the
-// set size is known (window path); the others wait for every workgroup's
-// "candidates written" tag (normally already set) and rank.
-__device__ __forceinline__ void rank_deferred(Ctx &C, const Defer &D) {
-    if (!D.active) return;
-    const BucketDesc &d = C.A.bk[D.b];
-    const uint32_t first_e = C.w * FNW;
-    if (D.nc != 0xffffffffu && first_e >= D.nc + (D.tail_cand && D.nc < CAND_CAP ? 1u : 0u)) return;
-    Lds &L = C.L;
-    const uint32_t nsw = (C.G + 63) / 64;
-    if (C.wave < nsw) {
-        const uint32_t tg = C.tag(D.b);
-        const uint32_t v = C.wave * 64 + C.flane();
-        bool pend = v < C.G;
-        for (uint32_t spins = 0;; ++spins) {
-            if (pend) pend = (uint32_t)(ld_sc1(&C.ctl()->cdone[D.b][v]) >> 32) != tg;
-            if (!__any(pend)) break;
+// The heap fill of bucket b, run by every ranker once the bucket's decision
+// is posted.
+__device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
+    const BucketDesc &d = C.A.bk[b];
+    const uint32_t lane = flane();
+    Decision &D = C.ctl()->dec[b];
+    const uint32_t tD = C.tag(TAG_DEC);
+    uint64_t w0 = ld_sc1(&D.w[0]);
+    for (uint32_t spins = 0; (uint32_t)(w0 >> 32) != tD; ++spins) {
+        __builtin_amdgcn_s_sleep(2);
+        w0 = ld_sc1(&D.w[0]);
+        if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); return; }
+    }
+    const uint32_t flags = uni((uint32_t)w0);
+    if (!(flags & DEC_B)) return;
+    const uint64_t w1 = ld_sc1(&D.w[1]), w2 = ld_sc1(&D.w[2]), w3 = ld_sc1(&D.w[3]);
+    const uint32_t cnt = uni((uint32_t)(w1 >> 32)), M = uni((uint32_t)w1);
+    const uint32_t Wtot = uni((uint32_t)(w2 >> 32));
+    const float tail_key = __uint_as_float(uni((uint32_t)w2));
+    const float t = __uint_as_float(uni((uint32_t)w3));
+    if (b < 8) C.stamp(64 + 4 * b, 0);
+    if (flags & DEC_WIN) {
+        // the window holds the top M; every chunk wrote its window lines at
+        // its exchanged offset -- wait for all of them, rank this share
+        // RK rankers per bucket (a rotating group, so the set is fetched RK
+        // times rather than G times)
+        const bool tail = (flags & DEC_TAIL) != 0;
+        const uint32_t NG = std::max(1u, C.G / RK);
+        const uint32_t g = b % NG;
+        if (C.w % NG != g) return;
+        const uint32_t R = (C.G - g + NG - 1) / NG, r = C.w / NG;
+        if (r >= Wtot + (tail ? 1u : 0u)) return;
+        BucketCtl *bc = &C.cc()->bk[b];
+        for (uint32_t spins = 0; ld_acq_relaxed(&bc->lists) < d.nc; ++spins) {
             __builtin_amdgcn_s_sleep(2);
-            if (spins > (1u << 22)) { atomicOr(C.fail(), (uint32_t)FAIL_SPIN_TIMEOUT); break; }
+            if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); return; }
         }
+        if (b < 8) C.stamp(64 + 4 * b + 1, 0);
+        rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
+    } else {
+        rank_rare(C, b, flags, cnt, M, t, tail_key);
     }
-    __syncthreads();
-    uint32_t nc_all = D.nc;
-    if (nc_all == 0xffffffffu) nc_all = uni(ld_acq_relaxed(&C.ctl()->cc[C.A.epoch & 1u].bk[D.b].cand_n));
-    if (nc_all > CAND_CAP) {
-        if (C.ftid() == 0) atomicOr(C.fail(), (uint32_t)FAIL_CAND_OVERFLOW);
-        nc_all = CAND_CAP;
-    }
-    (void)L;
-    rank_emit(C, d, C.cand() + (size_t)(D.b & 3u) * CAND_CAP, D.cnt, nc_all, D.tail_cand && nc_all < CAND_CAP,
-              D.tail_key);
+    if (b < 8) C.stamp(64 + 4 * b + 2, 0);
 }
 
-// STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = return
-// after the streaming passes; 2 = skip everything after the count exchanges;
-// 3 = plain streaming read (calibration); 4 = full codec + per-workgroup
-// s_memrealtime stamps: stamps[w*16 + 15] at start, [w*16 + 2b] after scan(b),
-// [w*16 + 2b + 1] after finish(b) and the deferred rank of b-1 (b < 7),
-// [w*16 + 14] = XCC id; 5 = full codec without the regime-B heap fill.
+// STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = the
+// streaming waves' work only (the finisher releases buffers at once);
+// 3 = plain streaming read (calibration); 4 = full codec + s_memrealtime
+// stamps (tools/stamps.py); 5 = full codec without the regime-B heap fill.
 template <int STAGE>
 __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
     __shared__ Lds L;
-    Ctx C{A, L, gridDim.x, blockIdx.x, (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6), 0,
-          false, A.ctl, A.cand, A.fail};
-    // STAGE 4: stamps go to LDS (a global store here would make the wave's
-    // next vmcnt wait include its write-back) and are flushed at the end
-    auto stamp = [&](uint32_t k) {
-        if (STAGE == 4 && C.ftid() == 0 && k < 16) L.stamp[k] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    };
-    if (STAGE == 4 && C.ftid() < 32) L.stamp[C.ftid()] = 0;
-    stamp(15);
-    if (STAGE == 4 && C.ftid() == 0) L.stamp[14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    Ctx C{A, L, gridDim.x, blockIdx.x, 0, A.ctl, A.cand, A.fail, STAGE == 4};
+    if (STAGE == 4 && threadIdx.x < 128) L.stamp[threadIdx.x] = 0;
     {  // zero the next call's per-call counters (this call never touches them)
         uint32_t *z = reinterpret_cast<uint32_t *>(&A.ctl->cc[(A.epoch + 1) & 1u]);
         constexpr uint32_t words = sizeof(CallCtl) / 4;
         const uint32_t per = (words + C.G - 1) / C.G;
         const uint32_t z0 = C.w * per, z1 = std::min(words, z0 + per);
-        for (uint32_t i = z0 + C.ftid(); i < z1; i += FWG) st_sc1(z + i, 0u);
+        for (uint32_t i = z0 + threadIdx.x; i < z1; i += FWG) st_sc1(z + i, 0u);
     }
-    // software pipeline: scan(b) | finish(b-LA) | deferred rank of b-LA-1
-    static_assert(LA == 2, "carry rotation below is written for LA == 2");
-    Carry ca{}, cb{}, cur{};  // scan results of buckets b-2, b-1, b (no indexed locals: no scratch)
-    Defer pend{};             // regime-B set awaiting its rank-and-emit
-    Prefetch pf{};            // granules of bucket b-LA, loaded during scan(b) (into Lds::pf)
-    for (uint32_t b = 0; b <= A.nbk + LA; ++b) {
-        // opaque per iteration: addresses derived from the workgroup id are
-        // recomputed (scalar) instead of hoisted into live vector registers
-        asm volatile("" : "+s"(C.w), "+s"(C.G), "+s"(C.ctlp), "+s"(C.candp), "+s"(C.failp));
-        if (b < A.nbk) {
-            // ranges beyond LINES_B keep their line sums in global scratch
-            if (C.range_len(A.bk[b]) <= LINES_B) cur = scan_bucket<STAGE, true>(C, b, pf);
-            else cur = scan_bucket<STAGE, false>(C, b, pf);
-            if (b < 7) stamp(2 * b);
+    if (threadIdx.x < NBUF) {
+        L.nst[threadIdx.x] = 0;
+        L.nwl[threadIdx.x] = 0;
+        L.qcnt[threadIdx.x] = 0;
+        L.wcnt[threadIdx.x] = 0;
+        L.sdone[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) {
+        L.fdone = 0;
+        // slots 0 and 1: chunks w and G + w; later slots take the next chunk
+        // of the call's counter (2G + n), so every workgroup's slots hold
+        // increasing chunks and chunks are taken in order
+        L.cid[0] = C.w;
+        L.cid[1] = C.G + C.w;
+        L.cseq = 2;
+    }
+    __syncthreads();
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave < NS) {
+        for (uint32_t j = 0;; ++j) {
+            for (uint32_t spins = 0; lds_ld(&L.cseq) <= j; ++spins) {
+                __builtin_amdgcn_s_sleep(1);
+                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+            }
+            const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
+            if (k >= A.K) break;
+            // wave 0 takes the chunk of slot j + 2 from the call's counter;
+            // the atomic returns while it streams slot j
+            uint32_t sq = 0, nx = 0;
+            bool grab = false;
+            if (wave == 0) {
+                sq = uni(lds_ld(&L.cseq));
+                grab = sq == j + 2 && uni(lds_ld(&L.cid[(sq - 1) % CIDR])) < A.K;
+                if (grab && flane() == 0) nx = 2 * C.G + atomicAdd(&C.cc()->next, 1u);
+            }
+            asm volatile("" : "+s"(C.w), "+s"(C.G));
+            scan_chunk<STAGE>(C, j, k, wave);
+            if (grab && flane() == 0) {
+                L.cid[sq % CIDR] = nx;
+                lds_drain();
+                lds_st(&L.cseq, sq + 1);
+            }
         }
-        if (STAGE == 1 || STAGE == 3) continue;
-        Defer dn{};
-        C.probe = STAGE == 4 && b == 2 + LA;
-        if (b >= LA && b - LA < A.nbk) dn = finish_bucket<STAGE>(C, b - LA, ca, pf);
-        C.sub(6);
-        rank_deferred(C, pend);
-        C.sub(7);
-        C.probe = false;
-        if (b >= LA && b - LA < 7) stamp(2 * (b - LA) + 1);
-        pend = dn;
-        ca = cb;
-        cb = cur;
-    }
-    if (STAGE == 4) {
-        __syncthreads();
-        if (C.ftid() < 16) A.stamps[C.w * 16 + C.ftid()] = L.stamp[C.ftid()];
-        else if (C.ftid() < 32) A.stamps[16 * 1024 + C.w * 16 + C.ftid() - 16] = L.stamp[C.ftid()];
+    } else if (wave == FIN) {
+        __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
+        FinState F{0};
+        for (uint32_t j = 0;; ++j) {
+            for (uint32_t spins = 0; lds_ld(&L.cseq) <= j; ++spins) {
+                __builtin_amdgcn_s_sleep(1);
+                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+            }
+            const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
+            if (k >= A.K) break;
+            asm volatile("" : "+s"(C.w), "+s"(C.G), "+s"(C.ctlp), "+s"(C.candp), "+s"(C.failp));
+            finish_chunk<STAGE>(C, j, k, F);
+        }
+        vm_drain();
+        flush_lists(C, F);
+    } else {
+        __builtin_amdgcn_s_setprio(2);
+        if (STAGE != 1 && STAGE != 3) {
+            for (uint32_t b = 0; b < A.nbk; ++b) {
+                asm volatile("" : "+s"(C.w), "+s"(C.G), "+s"(C.ctlp), "+s"(C.candp), "+s"(C.failp));
+                rank_bucket(C, b);
+            }
+        }
+        if (STAGE == 4) {
+            // the finisher and streamers are done with their stamps when every
+            // bucket is decided; the ranker flushes them last
+            for (uint32_t i = flane(); i < 128; i += 64) A.stamps[C.w * 128 + i] = L.stamp[i];
+        }
     }
 }
 
@@ -874,7 +1181,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     if (!a.nb) return hipSuccess;
     if (a.nb > MAX_BATCH || !a.epoch || a.epoch >= (1u << 24)) return hipErrorInvalidValue;
     BatchArgs A{};
-    uint32_t max_nb = 1;
+    uint32_t K = 0;
     for (uint32_t i = 0; i < a.nb; ++i) {
         const Tv16Bucket &b = a.b[i];
         if (b.first) {  // first threshold from sequential line sums (thresholdv16.cpp:36-54)
@@ -896,30 +1203,28 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         d.tl = (uint32_t)(b.n % 16);
         d.dst_len = b.dst_len;
         d.idx_offset = b.idx_offset;
-        max_nb = std::max(max_nb, d.nb);
+        d.cs = K;
+        d.nc = std::max<uint32_t>(1, (d.nb + TV16_CHUNK - 1) / TV16_CHUNK);
+        K += d.nc;
     }
+    if (K > a.desc_cap) return hipErrorInvalidValue;
     A.nbk = a.nb;
     A.epoch = a.epoch;
+    A.K = K;
     A.ctl = ws.ctl;
+    A.desc = ws.desc;
     A.cand = ws.cand;
     A.fail = ws.fail;
     A.stamps = a.b[a.nb - 1].count_out + 1;  // STAGE 4: words after the last bucket's count
     // wg_per_cu 1024-thread workgroups per CU (2: 32 waves, full occupancy for
     // one stream; 1: two launches from two streams share the CUs), all
-    // co-resident for the in-launch exchanges, >= 1024 lines of the largest
-    // bucket each
+    // co-resident for the in-launch exchanges; no more than there are chunks
     const uint32_t G = std::max<uint32_t>(
-        1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, (max_nb + 1023) / 1024),
-                              MAX_FILL_WG));
-    for (uint32_t i = 0; i < a.nb; ++i) {
-        A.bk[i].per = A.bk[i].nb / G;
-        A.bk[i].rem = A.bk[i].nb % G;
-    }
+        1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, K), MAXG));
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     switch (dbg_stage) {
         case 1: tv16_batch<1><<<G, FWG, 0, s>>>(A); break;
-        case 2: tv16_batch<2><<<G, FWG, 0, s>>>(A); break;
         case 3: tv16_batch<3><<<G, FWG, 0, s>>>(A); break;
         case 4: tv16_batch<4><<<G, FWG, 0, s>>>(A); break;
         case 5: tv16_batch<5><<<G, FWG, 0, s>>>(A); break;

@@ -13,7 +13,7 @@ constexpr uint32_t TV16_UNROLL = TV16_TILE_BLOCKS / (STG_WG / 4);  // 8 float4 p
 constexpr uint32_t HBINS = 1024;             // regime-B histogram bins per level
 constexpr uint32_t MAX_LEVELS = 6;           // regime-B radix-descent levels
 constexpr uint32_t CAND_CAP = 4096;          // regime-B candidates ranked in LDS per bucket
-constexpr uint32_t SORT_CAP = 4 * CAND_CAP;  // global candidate buffers: one per bucket % 4
+constexpr uint32_t SORT_CAP = 16 * CAND_CAP; // global candidate buffers: one per bucket of a launch
 constexpr uint32_t MAX_FILL_WG = 1024;       // upper bound on fill-kernel workgroups
 
 constexpr uint32_t TV_TILE = 8192;           // threshold-v elements per tile (32 KiB)
@@ -22,25 +22,24 @@ constexpr uint32_t TV_STAGE = 512;           // staged qualifiers per threshold-
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 
 // thresholdv16 in-launch control block (one launch = a batch of <= MAX_BATCH
-// buckets).  Per-call counters come in two copies selected by the call
-// epoch's parity; every launch zeroes the other copy for the next call (the
-// next call on this workspace is stream-ordered after this launch).  Words
-// handed between workgroups carry a 32-bit tag {epoch:24 | bucket:8}.  The
-// count granules and "candidates written" tags are per bucket (a fast
-// workgroup may publish bucket b+2 while a slow one still gathers bucket b).
-// Regime-B candidates of bucket b are written in finish(b) (after scan(b+1))
-// and read in the deferred rank after scan(b+2); a workgroup can be writing
-// bucket b's set while a slow one still ranks b-1 or b-2 but never b-3, so the
-// candidate buffers and tie counts rotate over bucket % 4.
+// buckets cut into fixed 2048-line chunks).  Per-call counters come in two
+// copies selected by the call epoch's parity; every launch zeroes the other
+// copy for the next call (the next call on this workspace is stream-ordered
+// after this launch).  Words handed between workgroups carry the call tag
+// (epoch << 8 | kind) so stale words of earlier calls never match.
+// Regime-B candidate sets: one CAND_CAP slot per bucket of the launch.
 constexpr uint32_t MAX_BATCH = 16;
+constexpr uint32_t TV16_CHUNK = 2048;        // lines (16 floats) per chunk = 128 KiB
 struct BucketCtl {
-    uint32_t cand_n;    // regime-B candidates appended (histogram paths only)
-    uint32_t pad[3];
+    uint32_t cand_n;    // regime-B candidates appended (rare paths only)
+    uint32_t lists;     // chunks whose window lists are in place
+    uint32_t pad[2];
     uint32_t hist[MAX_LEVELS][HBINS];
 };
 struct CallCtl {
     uint32_t bar;       // grid-barrier arrivals (round r completes at r * G)
-    uint32_t pad[3];
+    uint32_t next;      // dynamic chunk counter
+    uint32_t pad[2];
     BucketCtl bk[MAX_BATCH];
 };
 // One 128-byte line per workgroup, written by a barrier's last arriver and
@@ -49,14 +48,20 @@ struct alignas(128) WgSlot {
     uint64_t go;        // {epoch tag:32 | barrier round:32}
     uint64_t pad[15];
 };
+// Per-bucket regime decision, written by the finisher of the bucket's first
+// chunk: [1..3] first, drained, then [0] = {tag:32 | flags:32}.
+struct alignas(32) Decision {
+    uint64_t w[4];      // [1] = {cnt:32 | M:32}, [2] = {Wtot:32 | tail key bits:32}, [3] = {Qtot:32 | t bits:32}
+};
 struct FillCtl {
     CallCtl cc[2];                     // [epoch parity]
-    uint32_t wg_ties[4][MAX_FILL_WG];  // [bucket % 4] regime-B ties per workgroup
-    // per bucket and workgroup: [0] = {tag:32 | qualifying lines:32},
-    // [1] = {tag:32 | window lines:32}; 16 B so one lane fetches both
-    uint64_t gran[MAX_BATCH][MAX_FILL_WG][2];
-    uint64_t cdone[MAX_BATCH][MAX_FILL_WG];  // {tag:32 | 0}: regime-B candidates written
+    Decision dec[MAX_BATCH];
     WgSlot slot[MAX_FILL_WG];
+};
+// Per-chunk descriptor (16 B): every word carries the call tag.
+struct alignas(16) ChunkDesc {
+    uint64_t agg;       // {tag:32 | qualifying lines:16 | window lines:16}, by the last streaming wave
+    uint64_t ties;      // {tag:32 | lines tied at u* (regime-B rare path)}
 };
 
 // Per-call scalars handed from the scan kernel to the fill kernel.
@@ -77,10 +82,11 @@ struct RSel {
 
 struct DevWS {
     FillCtl *ctl;
+    ChunkDesc *desc;     // thresholdv16 chunk descriptors (grown per launch, zeroed)
     CallParams *cp;
     RSel *rsel;
     uint32_t *fail;      // sticky failure bits
-    uint64_t *cand;      // regime-B candidates (key << 32 | pos), CAND_CAP per bucket % 4
+    uint64_t *cand;      // regime-B candidates (key << 32 | pos), CAND_CAP per bucket of a launch
     uint32_t *misc;      // small scratch (counts)
     float *sums;         // thresholdv16: one sum per 16-float line
     uint32_t *tile_cnt;  // per-tile qualifier counts
@@ -110,6 +116,7 @@ struct Tv16Launch {
     hipEvent_t *ev;    // optional [before, mid, after] the codec launch(es)
     uint32_t epoch;    // per-workspace call counter, 1..2^24-1 (hand-off tags)
     uint32_t wg_per_cu;  // fused-kernel workgroups per CU (1 or 2)
+    uint32_t desc_cap;   // ChunkDesc entries at ws.desc
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
 

@@ -44,6 +44,20 @@ for s in "$@"; do
             unset STG_DEBUG_TV16_STAGE ;;
         ubench) step ubench 300 python tools/ubench_read.py ;;
         configs) step configs 500 python tools/bench_configs.py ;;
+        depths)  # tuning variants built as stellatrain_amd/libstg_codec_d*.so
+            for L in stellatrain_amd/libstg_codec_*.so; do
+                v=$(basename $L .so); v=${v#libstg_codec_}
+                export STG_CODEC_LIB=$R/$L
+                step depth_$v 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline
+                if [ -n "${DEPTH_STAGES:-}" ]; then
+                    for st in $DEPTH_STAGES; do
+                        export STG_DEBUG_TV16_STAGE=$st
+                        step depth_${v}_s$st 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline
+                        unset STG_DEBUG_TV16_STAGE
+                    done
+                fi
+                unset STG_CODEC_LIB
+            done ;;
         sweep)
             for W in 1 2; do for S in 1 2; do for K in 8 16; do
                 export STG_TV16_WGPERCU=$W

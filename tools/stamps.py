@@ -1,11 +1,16 @@
 #!/usr/bin/env python3
 """Phase timeline of the batched thresholdv16 kernel (diagnostic build).
 
-Run with STG_DEBUG_TV16_STAGE=4: every workgroup writes s_memrealtime
-(100 MHz) at its start (slot 15), after scan(b) (slot 2b) and after finish(b)
-(slot 2b+1), b < 7, into the words after the last bucket's count.  Prints,
-per bucket, the critical-path time (max over workgroups, relative to the
-earliest start) of each boundary, and the median, in microseconds.
+Run with STG_DEBUG_TV16_STAGE=4: every workgroup records s_memrealtime
+(100 MHz) into 128 words after the last bucket's count:
+  [j*8 + 0]  finisher, slot j < 8: the streaming waves are done with the chunk
+  [j*8 + 1]  finisher: look-back done (prefix known, inclusive published)
+  [j*8 + 2]  finisher: chunk emitted, window list written, slot released
+  [64 + 4b]      ranker, bucket b < 8 (regime B only): decision seen
+  [64 + 4b + 1]  ranker: every chunk's window list in place
+  [64 + 4b + 2]  ranker: heap fill share emitted
+Prints medians / maxima over workgroups (microseconds from the earliest stamp
+of the call), median over calls.
 """
 from __future__ import annotations
 
@@ -28,9 +33,9 @@ def main():
     from stellatrain_amd._capi import check, lib
     from stellatrain_amd.synth import seed_for
     dev = torch.device("cuda", 0)
-    n = 16 << 20
+    n = int(os.environ.get("STAMPS_MIB", "64")) * (1 << 18)
     k = merge_numel(n, 0.99)
-    nb = int(os.environ.get("STAMPS_BUCKETS", "7"))
+    nb = int(os.environ.get("STAMPS_BUCKETS", "8"))
     comp = ThresholdvCompressor16()
     st = torch.cuda.current_stream(dev)
     bufs = []
@@ -41,7 +46,7 @@ def main():
         bufs.append(t)
     outs = [(torch.zeros(k, dtype=torch.int32, device=dev), torch.zeros(k, dtype=torch.float32, device=dev))
             for _ in range(nb)]
-    cnt = torch.zeros(nb + 2 * 1024 * 16, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(nb + 1024 * 128, dtype=torch.int32, device=dev)
     counts = cnt[:nb]
 
     def call(s):
@@ -49,55 +54,42 @@ def main():
                                           for i in range(nb)], counts=counts)
     call(0)
     torch.cuda.synchronize()
-    rows = []
-    for s in range(1, 25):
+    per_call = []
+    for s in range(1, 21):
         cnt[nb:].zero_()
         call(s)
         torch.cuda.synchronize()
-        all_ = cnt[nb:].cpu().numpy().view(np.uint32).astype(np.int64)
-        a = all_[:16 * 1024].reshape(1024, 16)
-        p = all_[16 * 1024:].reshape(1024, 16)
-        used = a[:, 15] != 0
-        a, p = a[used], p[used]
-        t0 = a[:, 15].min()
-        rel = (a[:, :14] - t0) / 100.0
-        # probe: finish(2) after scan(3): 1 start, 2 gathered, 3 emitted, 4 AIMD
-        # written, 5 regime-B collected, 6 finish end, 7 rank_deferred(1) end
-        base = p[:, 1]
-        sub = np.where(p[:, 1:8] > 0, (p[:, 1:8] - base[:, None]) / 100.0, np.nan)
-        regime_b = bool((p[:, 5] > 0).any())
-        stale = p[:, 8]  # probe: lanes stale at the first gather check, max poll rounds
-        polls = p[:, 9]
-        xcc = a[:, 14] & 0xF
-        scan0 = rel[:, 0]
-        per_xcc = [float(np.median(scan0[xcc == x])) if (xcc == x).any() else np.nan for x in range(8)]
-        wg_ids = np.nonzero(used)[0]
-        slow = wg_ids[np.argsort(scan0)[-16:]]
-        rows.append({"xcc_scan0": per_xcc, "slow_wgs": slow.tolist(), "slow_xcc": xcc[np.argsort(scan0)[-16:]].tolist(),
-                     "crit": rel.max(axis=0), "med": np.median(rel, axis=0),
-                     "start_spread": float((a[:, 15].max() - t0) / 100.0), "wgs": int(used.sum()),
-                     "sub_med": np.nanmedian(sub, axis=0), "stale_wgs": int((stale > 0).sum()),
-                     "stale_lanes_max": int(stale.max()), "polls_max": int(polls.max()), "sub_max": np.nanmax(sub, axis=0), "B": regime_b})
-    crit = np.median(np.stack([r["crit"] for r in rows]), axis=0)
-    med = np.median(np.stack([r["med"] for r in rows]), axis=0)
-    out = {"buckets": nb, "wgs": rows[0]["wgs"],
-           "start_spread_us": round(float(np.median([r["start_spread"] for r in rows])), 2),
-           "scan_end_crit_us": [round(float(crit[2 * b]), 2) for b in range(min(nb, 7))],
-           "finish_end_crit_us": [round(float(crit[2 * b + 1]), 2) for b in range(min(nb, 7))],
-           "scan_end_median_us": [round(float(med[2 * b]), 2) for b in range(min(nb, 7))],
-           "finish_end_median_us": [round(float(med[2 * b + 1]), 2) for b in range(min(nb, 7))]}
-    out["scan0_median_by_xcc_us"] = [round(float(x), 2) for x in np.nanmedian(np.stack([r["xcc_scan0"] for r in rows]), 0)]
-    out["slowest16_wgs_call1"] = rows[0]["slow_wgs"]
-    out["slowest16_xcc_call1"] = rows[0]["slow_xcc"]
-    out["slowest16_wgs_call2"] = rows[1]["slow_wgs"]
-    for tag in (False, True):
-        rr = [r for r in rows if r["B"] == tag]
-        if rr:
-            out["probe_" + ("B" if tag else "A")] = {
-                "calls": len(rr), "stale_wgs": [r["stale_wgs"] for r in rr][:6],
-                "stale_lanes_max": [r["stale_lanes_max"] for r in rr][:6], "polls_max": [r["polls_max"] for r in rr][:6],
-                "sub_median_us": [round(float(x), 2) for x in np.nanmedian(np.stack([r["sub_med"] for r in rr]), 0)],
-                "sub_max_us": [round(float(x), 2) for x in np.nanmedian(np.stack([r["sub_max"] for r in rr]), 0)]}
+        a = cnt[nb:].cpu().numpy().view(np.uint32).astype(np.int64).reshape(1024, 128)
+        used = (a != 0).any(axis=1)
+        a = a[used]
+        t0 = np.where(a > 0, a, np.iinfo(np.int64).max).min()
+        per_call.append(np.where(a > 0, (a - t0) / 100.0, np.nan))
+    stack = np.stack(per_call)  # calls x wgs x 128
+
+    def med(slot):
+        x = stack[:, :, slot]
+        return round(float(np.nanmedian(np.nanmedian(x, axis=1))), 2) if np.isfinite(x).any() else None
+
+    def mx(slot):
+        x = stack[:, :, slot]
+        return round(float(np.nanmedian(np.nanmax(x, axis=1))), 2) if np.isfinite(x).any() else None
+
+    def dur(s1, s0):
+        x = stack[:, :, s1] - stack[:, :, s0]
+        return round(float(np.nanmedian(x)), 2) if np.isfinite(x).any() else None
+
+    out = {"buckets": nb, "wgs": int(stack.shape[1]), "calls": len(per_call)}
+    out["slot_ready_med"] = [med(j * 8) for j in range(8)]
+    out["slot_ready_max"] = [mx(j * 8) for j in range(8)]
+    out["slot_released_med"] = [med(j * 8 + 2) for j in range(8)]
+    out["slot_released_max"] = [mx(j * 8 + 2) for j in range(8)]
+    out["lookback_us_med"] = [dur(j * 8 + 1, j * 8) for j in range(8)]
+    out["emit_us_med"] = [dur(j * 8 + 2, j * 8 + 1) for j in range(8)]
+    out["rank_decision_med"] = [med(64 + 4 * b) for b in range(8)]
+    out["rank_lists_in_med"] = [med(64 + 4 * b + 1) for b in range(8)]
+    out["rank_done_med"] = [med(64 + 4 * b + 2) for b in range(8)]
+    out["rank_done_max"] = [mx(64 + 4 * b + 2) for b in range(8)]
+    out["rank_emit_us_med"] = [dur(64 + 4 * b + 2, 64 + 4 * b + 1) for b in range(8)]
     print(json.dumps(out))
 
 
