@@ -40,17 +40,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=8)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--mib", type=int, default=64)
     p.add_argument("--ratio", type=float, default=0.99)
-    p.add_argument("--keys", type=int, default=8)
+    p.add_argument("--keys", type=int, default=16)
     p.add_argument("--method", default="thresholdv16")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", type=int, default=16)
-    p.add_argument("--streams", type=int, default=1,
-                   help="issue key i's calls on stream i %% S, like the engine's worker pool")
+    p.add_argument("--streams", type=int, default=2,
+                   help="issue key i's calls on stream i %% S, like the engine's worker pool; with S > 1 each "
+                        "persistent launch takes one workgroup per CU so two launches share the chip")
     return p.parse_args()
 
 
@@ -92,6 +93,10 @@ def load_traffic(buckets_per_launch: int):
 
 def main():
     args = parse()
+    if args.streams > 1:
+        # two concurrent persistent launches (one 1024-thread workgroup per CU
+        # each): one launch's exchange tail overlaps the other's streaming
+        os.environ.setdefault("STG_TV16_WGPERCU", "1")
     import torch
     import torch.distributed as dist
 

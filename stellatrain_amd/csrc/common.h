@@ -143,17 +143,33 @@ __device__ __forceinline__ uint64_t blk_sum64(uint64_t v, uint64_t *sh) {
 // inside one launch (MI355X_MICROARCH "Valid forms", row 1): no release or
 // acquire fence is needed when every store and every load of the bytes is sc1
 // and the storing waves drain before the counter add.
+//
+// Every helper casts to the global address space: a pointer that lost its
+// address space (e.g. through an opaque register launder) would otherwise
+// become a flat access, which counts against lgkmcnt as well as vmcnt, so the
+// next LDS wait would also wait for the memory round trip.
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *gp(T *p) {
+    return (__attribute__((address_space(1))) T *)p;
+}
 __device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
-    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gp(const_cast<uint64_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
-    return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gp(const_cast<uint32_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Global (agent-scope, relaxed) atomic add / or; return the old value.
+__device__ __forceinline__ uint32_t g_add(uint32_t *p, uint32_t v) {
+    return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t g_or(uint32_t *p, uint32_t v) {
+    return __hip_atomic_fetch_or(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fence-free grid barrier for sc1/atomic-only hand-offs: every wave drains its
@@ -178,7 +194,7 @@ __device__ __forceinline__ void grid_barrier_sc1(uint32_t *ctr, uint32_t target,
 //     at agent scope then bumps a relaxed agent counter; consumer = one lane
 //     polls relaxed with s_sleep (bounded), one agent acquire, barrier. ---
 __device__ __forceinline__ uint32_t ld_acq_relaxed(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(gp(const_cast<uint32_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void release_prologue() {

@@ -65,9 +65,11 @@ static_assert(RNK == FNW - 1, "one streaming group, one finisher, one ranker");
 #endif
 constexpr uint32_t NBUF = STG_TV16_NBUF;  // LDS buffer sets (slots) in flight per workgroup
 constexpr uint32_t CIDR = 2 * NBUF;       // chunk-id ring
-constexpr uint32_t MAX_STEPS = TV16_CHUNK / 16;  // wave steps (16 lines) of a chunk
 constexpr uint32_t STAGE_B = 88;    // qualifying lines staged in LDS per slot (~20 expected at 1%)
 constexpr uint32_t WL_B = 64;       // window candidates listed in LDS per slot
+#ifndef STG_TV16_PRIO
+#define STG_TV16_PRIO 1
+#endif
 #ifndef STG_TV16_RK
 #define STG_TV16_RK 64
 #endif
@@ -149,7 +151,6 @@ struct Lds {
     // streaming waves -> finisher, by buffer set (slot % NBUF)
     float4 stage[NBUF][STAGE_B * 4];     // staged qualifying lines (64 B each)
     uint32_t stage_line[NBUF][STAGE_B];
-    uint64_t qm[NBUF][MAX_STEPS];        // per wave step (16 lines): qualifying ballot (bits at quad leaders)
     uint64_t wl[NBUF][WL_B];             // window candidates, composite keys
     uint32_t nst[NBUF];                  // qualifying lines staged (slot counter)
     uint32_t nwl[NBUF];                  // window candidates listed (slot counter)
@@ -158,11 +159,11 @@ struct Lds {
     uint32_t sdone[NBUF];                // streaming waves done with the chunk
     float tval[NBUF], incv[NBUF];        // the bucket's threshold state as scanned
     uint32_t cid[CIDR];                  // chunk of slot j at [j % CIDR] (>= K: no more chunks)
-    uint32_t cseq;                       // slots whose chunk id is known
+    uint32_t cok[CIDR];                  // j + 1 once cid[j % CIDR] holds slot j's chunk
+    uint32_t mid[CIDR];                  // waves past the middle of slot j (j % CIDR)
     uint32_t fdone;                      // slots released by the finisher
     // finisher
     uint4 gb[GB];                        // gathered chunk descriptors (one piece of a bucket)
-    uint32_t wt[MAX_STEPS];              // exclusive popcounts of qm[par][]
     // ranker
     union {
         uint64_t cand[CAND_CAP];         // rare path: candidate set (u64 composite keys)
@@ -284,7 +285,7 @@ struct Ctx {
     __device__ __forceinline__ FillCtl *ctl() const { return ctlp; }
     __device__ __forceinline__ CallCtl *cc() const { return &ctlp->cc[A.epoch & 1u]; }
     __device__ __forceinline__ uint64_t *cand(uint32_t b) const { return candp + (size_t)b * CAND_CAP; }
-    __device__ __forceinline__ void fail(uint32_t bits) const { atomicOr(failp, bits); }
+    __device__ __forceinline__ void fail(uint32_t bits) const { g_or(failp, bits); }
     __device__ __forceinline__ void stamp(uint32_t slot, uint32_t v) const {
         if (stamping && slot < 128 && flane() == 0) L.stamp[slot] = v ? v : (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
@@ -305,7 +306,7 @@ struct Ctx {
         const uint32_t lane = flane();
         vm_drain();
         uint32_t old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(&cc()->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) old = g_add(&cc()->bar, 1u);
         old = uni(old);
         if (old == r * G - 1) {
             for (uint32_t i = lane; i < G; i += 64) st_sc1(&fc->slot[i].go, go);
@@ -332,10 +333,12 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     Lds &L = C.L;
     const uint32_t par = j % NBUF;
     if (j >= NBUF) {  // buffer set `par` is free once the finisher released slot j - NBUF
-        for (uint32_t spins = 0; lds_ld(&L.fdone) < j + 1 - NBUF; ++spins) {
+        uint32_t spins = 0;
+        for (; lds_ld(&L.fdone) < j + 1 - NBUF; ++spins) {
             __builtin_amdgcn_s_sleep(2);
             if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
         }
+        if (C.stamping && spins && flane() == 0) atomicAdd(&L.stamp[120], spins);
     }
     const uint32_t b = C.bucket_of(k);
     const BucketDesc &d = C.A.bk[b];
@@ -368,7 +371,21 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     float4 v[SCAN_D];
 #pragma unroll
     for (uint32_t u = 0; u < SCAN_D; ++u) v[u] = load(u);
+    // The first wave past the middle of slot j takes the chunk of slot j + 2
+    // from the call's counter (slots 0 and 1 are static): late enough that
+    // chunks are taken close to when they are streamed (the finishers' prefix
+    // counts wait on earlier chunks only), early enough that the round trip
+    // hides behind the second half of the slot.
+    uint32_t nx = 0;
+    bool grab = false, tried = false;
     for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
+        if (!tried && m0 >= mine / 2) {
+            tried = true;
+            uint32_t first = 1;
+            if (flane() == 0) first = atomicAdd(&L.mid[j % CIDR], 1u);
+            grab = uni(first) == 0;
+            if (grab && flane() == 0) nx = 2 * C.G + g_add(&C.cc()->next, 1u);
+        }
 #pragma unroll
         for (uint32_t u = 0; u < SCAN_D; ++u) {
             const float4 x = v[u];
@@ -382,20 +399,22 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
             }
             const float S = quad_line_sum(x);  // the same in all four lanes of the quad
             v[u] = load(m0 + u + SCAN_D);
-            const bool in = i < nl;
-            const bool lead = in && q == 0;
             const uint32_t us = f2u(S);
-            const bool qual = in && S >= t;
+            // one test for the common case: no line of the step reaches the
+            // window [wlo, tb) or the threshold (sums are >= +0, so us >= tb
+            // iff S >= t for every non-NaN S)
+            const bool near = i < nl && us >= wlo;
+            if (!__ballot(near && q == 0)) continue;
+            const bool qual = near && S >= t;
+            const bool win = near && us < tb;
             const uint64_t bq = __ballot(qual && q == 0);
-            if (lane == 0 && i < nl) L.qm[par][i >> 4] = bq;
-            const bool win = lead && us >= wlo && us < tb;
-            const uint64_t bw = __ballot(win);
+            const uint64_t bw = __ballot(win && q == 0);
             if (bw) {  // list the window candidates (composite keys)
                 win_w += (uint32_t)__popcll(bw);
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&L.nwl[par], (uint32_t)__popcll(bw));
                 base = __builtin_amdgcn_readfirstlane(base);
-                if (win) {
+                if (win && q == 0) {
                     const uint32_t slot = base + (uint32_t)__popcll(bw & below_mask(flane()));
                     if (slot < WL_B) L.wl[par][slot] = cand_key(us, (L0 + i) * 16);
                 }
@@ -419,6 +438,20 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
                 }
             }
         }
+    }
+    if (!tried && mine == 0 && s == 0) {  // an empty chunk: wave 0 takes it
+        uint32_t first = 1;
+        if (flane() == 0) first = atomicAdd(&L.mid[j % CIDR], 1u);
+        grab = uni(first) == 0;
+        if (grab && flane() == 0) nx = 2 * C.G + g_add(&C.cc()->next, 1u);
+    }
+    if (grab && flane() == 0) {
+        // slot j + NBUF reuses slot j - NBUF's counter: every wave is done
+        // with slot j - NBUF (the finisher released it) and none is past j yet
+        L.mid[(j + NBUF) % CIDR] = 0;
+        L.cid[(j + 2) % CIDR] = nx;
+        lds_drain();
+        lds_st(&L.cok[(j + 2) % CIDR], j + 3);
     }
     if (lane == 0) {
         if (cnt_w) atomicAdd(&L.qcnt[par], cnt_w);
@@ -473,7 +506,7 @@ __device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, ui
             if (i < n) { const uint4 e = L.gb[i]; a = ((uint64_t)e.y << 32) | e.x; }
             bool pend = i < n && (uint32_t)(a >> 32) != tA;
             for (uint32_t spins = 0; __any(pend); ++spins) {
-                __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_s_sleep(4);  // a poll is a memory round trip: do not flood the queues
                 if (pend) {
                     a = ld_sc1(&C.A.desc[d.cs + p0 + i].agg);
                     pend = (uint32_t)(a >> 32) != tA;
@@ -497,7 +530,7 @@ struct FinState {
 __device__ __forceinline__ void flush_lists(Ctx &C, FinState &F) {
     for (uint32_t b = 0; F.pend; ++b, F.pend >>= 4) {
         const uint32_t n = (uint32_t)(F.pend & 15u);
-        if (n && flane() == 0) atomicAdd(&C.cc()->bk[b].lists, n);
+        if (n && flane() == 0) g_add(&C.cc()->bk[b].lists, n);
     }
 }
 
@@ -509,6 +542,12 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
     Lds &L = C.L;
     const uint32_t par = j % NBUF;
     const uint32_t lane = flane();
+    if (F.pend && lds_ld(&L.sdone[par]) < NS) {
+        // idle until the chunk is streamed: retire and count the pending
+        // window lists now (the rankers wait for them)
+        vm_drain();
+        flush_lists(C, F);
+    }
     for (uint32_t spins = 0; lds_ld(&L.sdone[par]) < NS; ++spins) {
         __builtin_amdgcn_s_sleep(1);
         if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
@@ -524,7 +563,7 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
     const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
     const uint32_t qw = uni(L.qcnt[par]);
     const float t = uni(L.tval[par]), inc = uni(L.incv[par]);
-    if (j < 8) C.stamp(j * 8 + 0, 0);
+    if (j < 16) C.stamp(j * 4 + 0, 0);
 
     // ---- prefix counts of the bucket's earlier chunks ----
     uint32_t P = 0, Wbef = 0;
@@ -533,33 +572,24 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
         flush_lists(C, F);  // the gather retired the earlier chunks' list stores
     }
     const uint32_t ww = uni(L.wcnt[par]);
-    if (j < 8) C.stamp(j * 8 + 1, 0);
+    if (j < 16) C.stamp(j * 4 + 1, 0);
 
     // ---- ordered emission of the chunk's qualifying lines with rank < lim ----
     const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
     const uint32_t lim = kb + (r ? 1u : 0u);
     const bool vec = aligned16(d);
     if (P < lim && qw) {
-        // in-chunk rank from the streaming waves' per-step ballots (bits at 4 * line)
-        const uint32_t nsteps = (nl + 15) / 16;
-        {
-            const uint32_t j0 = 2 * lane, j1 = 2 * lane + 1;
-            const uint32_t c0s = j0 < nsteps ? (uint32_t)__popcll(L.qm[par][j0]) : 0u;
-            const uint32_t c1s = j1 < nsteps ? (uint32_t)__popcll(L.qm[par][j1]) : 0u;
-            const uint32_t ex = wave_incl_scan(c0s + c1s) - (c0s + c1s);
-            L.wt[j0] = ex;
-            L.wt[j1] = ex + c0s;
-        }
-        lds_drain();
         if (qw <= STAGE_B) {
-            // every qualifying line is staged in LDS: a quad per line
+            // every qualifying line is staged in LDS with its line index: its
+            // in-chunk rank is the number of staged lines before it; a quad
+            // of lanes per line
             const uint32_t q = lane & 3;
             for (uint32_t e0 = 0; e0 < qw; e0 += 16) {
                 const uint32_t e = e0 + (lane >> 2);
                 if (e >= qw) continue;
                 const uint32_t i = L.stage_line[par][e];
-                const uint32_t jj = i >> 4, ln = (i & 15) * 4;
-                const uint32_t g = P + L.wt[jj] + (uint32_t)__popcll(L.qm[par][jj] & below_mask(ln));
+                uint32_t g = P;
+                for (uint32_t x = 0; x < qw; ++x) g += L.stage_line[par][x] < i;
                 if (g >= lim) continue;
                 const uint32_t pos = (L0 + i) * 16 + 4 * q;
                 const uint32_t len = g == kb ? r : 16u;
@@ -581,16 +611,18 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
                 }
             }
         } else {
-            // staging overflowed (low threshold): the ballots name the lines,
-            // src supplies the data
-            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+            // staging overflowed (low threshold): find the qualifying lines
+            // again from src (bit-identical line sums), in order
+            uint32_t base = P;
+            for (uint32_t i0 = 0; i0 < nl && base < lim; i0 += 64) {
                 const uint32_t i = i0 + lane;
-                const uint32_t jj = i >> 4, ln = (i & 15) * 4;
-                const uint64_t m = i < nl ? L.qm[par][jj] : 0ull;
-                if ((m >> ln) & 1ull) {
-                    const uint32_t g = P + L.wt[jj] + (uint32_t)__popcll(m & below_mask(ln));
+                const bool f = i < nl && lane_line_sum(d.src + (size_t)(L0 + i) * 16) >= t;
+                const uint64_t m = __ballot(f);
+                if (f) {
+                    const uint32_t g = base + (uint32_t)__popcll(m & below_mask(lane));
                     if (g < lim) emit_line(d, vec, (L0 + i) * 16, 16 * g, g == kb ? r : 16u);
                 }
+                base += (uint32_t)__popcll(m);
             }
         }
     }
@@ -639,7 +671,7 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
     }
     F.pend += 1ull << (4 * b);
     release(C, par, j);
-    if (j < 8) C.stamp(j * 8 + 2, 0);
+    if (j < 16) C.stamp(j * 4 + 2, 0);
 
     // ---- the bucket's last chunk: regime, tail, AIMD, count, decision ----
     if (c + 1 == d.nc) {
@@ -880,7 +912,7 @@ __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, ui
         lds_drain();
         for (uint32_t i = lane; i < HBINS; i += 64) {
             const uint32_t h = L.hist[i];
-            if (h) atomicAdd(&bc->hist[0][i], h);
+            if (h) g_add(&bc->hist[0][i], h);
         }
         C.grid_sync();
         uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
@@ -953,7 +985,7 @@ __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, ui
             lds_drain();
             for (uint32_t i = lane; i < HBINS; i += 64) {
                 const uint32_t h = L.hist[i];
-                if (h) atomicAdd(&bc->hist[lvl][i], h);
+                if (h) g_add(&bc->hist[lvl][i], h);
             }
             C.grid_sync();
         }
@@ -973,7 +1005,7 @@ __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, ui
         });
         mine = uni(wave_sum(mine));
         uint32_t o = 0;
-        if (lane == 0 && mine) o = atomicAdd(&bc->cand_n, mine);
+        if (lane == 0 && mine) o = g_add(&bc->cand_n, mine);
         uint32_t base = uni(o);
         for (uint32_t c = w; c < d.nc; c += G) {
             const uint32_t L0 = c * TV16_CHUNK;
@@ -1060,7 +1092,7 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
     const uint32_t Wtot = uni((uint32_t)(w2 >> 32));
     const float tail_key = __uint_as_float(uni((uint32_t)w2));
     const float t = __uint_as_float(uni((uint32_t)w3));
-    if (b < 8) C.stamp(64 + 4 * b, 0);
+    if (b < 16) C.stamp(64 + 4 * b, 0);
     if (flags & DEC_WIN) {
         // the window holds the top M; every chunk wrote its window lines at
         // its exchanged offset -- wait for all of them, rank this share
@@ -1077,12 +1109,12 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
             __builtin_amdgcn_s_sleep(2);
             if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); return; }
         }
-        if (b < 8) C.stamp(64 + 4 * b + 1, 0);
+        if (b < 16) C.stamp(64 + 4 * b + 1, 0);
         rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
     } else {
         rank_rare(C, b, flags, cnt, M, t, tail_key);
     }
-    if (b < 8) C.stamp(64 + 4 * b + 2, 0);
+    if (b < 16) C.stamp(64 + 4 * b + 2, 0);
 }
 
 // STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = the
@@ -1110,45 +1142,35 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
     }
     if (threadIdx.x == 0) {
         L.fdone = 0;
-        // slots 0 and 1: chunks w and G + w; later slots take the next chunk
-        // of the call's counter (2G + n), so every workgroup's slots hold
-        // increasing chunks and chunks are taken in order
+        // slots 0 and 1: chunks w and G + w; later slots take the next chunks
+        // of the call's counter (2G + n, taken by the finisher), so every
+        // workgroup's slots hold increasing chunks and chunks are taken in order
         L.cid[0] = C.w;
         L.cid[1] = C.G + C.w;
-        L.cseq = 2;
+        for (uint32_t i = 0; i < CIDR; ++i) { L.cok[i] = 0; L.mid[i] = 0; }
+        L.cok[0] = 1;
+        L.cok[1] = 2;
     }
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave < NS) {
         for (uint32_t j = 0;; ++j) {
-            for (uint32_t spins = 0; lds_ld(&L.cseq) <= j; ++spins) {
+            uint32_t spins = 0;
+            for (; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
                 if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
             }
+            if (C.stamping && spins && flane() == 0) atomicAdd(&L.stamp[121], spins);
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
             if (k >= A.K) break;
-            // wave 0 takes the chunk of slot j + 2 from the call's counter;
-            // the atomic returns while it streams slot j
-            uint32_t sq = 0, nx = 0;
-            bool grab = false;
-            if (wave == 0) {
-                sq = uni(lds_ld(&L.cseq));
-                grab = sq == j + 2 && uni(lds_ld(&L.cid[(sq - 1) % CIDR])) < A.K;
-                if (grab && flane() == 0) nx = 2 * C.G + atomicAdd(&C.cc()->next, 1u);
-            }
             asm volatile("" : "+s"(C.w), "+s"(C.G));
             scan_chunk<STAGE>(C, j, k, wave);
-            if (grab && flane() == 0) {
-                L.cid[sq % CIDR] = nx;
-                lds_drain();
-                lds_st(&L.cseq, sq + 1);
-            }
         }
     } else if (wave == FIN) {
-        __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
+        if (STG_TV16_PRIO) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
         FinState F{0};
         for (uint32_t j = 0;; ++j) {
-            for (uint32_t spins = 0; lds_ld(&L.cseq) <= j; ++spins) {
+            for (uint32_t spins = 0; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
                 if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
             }
@@ -1160,7 +1182,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
         vm_drain();
         flush_lists(C, F);
     } else {
-        __builtin_amdgcn_s_setprio(2);
+        if (STG_TV16_PRIO) __builtin_amdgcn_s_setprio(2);
         if (STAGE != 1 && STAGE != 3) {
             for (uint32_t b = 0; b < A.nbk; ++b) {
                 asm volatile("" : "+s"(C.w), "+s"(C.G), "+s"(C.ctlp), "+s"(C.candp), "+s"(C.failp));

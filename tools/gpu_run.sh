@@ -48,11 +48,11 @@ for s in "$@"; do
             for L in stellatrain_amd/libstg_codec_*.so; do
                 v=$(basename $L .so); v=${v#libstg_codec_}
                 export STG_CODEC_LIB=$R/$L
-                step depth_$v 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline
+                step depth_$v 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-}
                 if [ -n "${DEPTH_STAGES:-}" ]; then
                     for st in $DEPTH_STAGES; do
                         export STG_DEBUG_TV16_STAGE=$st
-                        step depth_${v}_s$st 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline
+                        step depth_${v}_s$st 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-}
                         unset STG_DEBUG_TV16_STAGE
                     done
                 fi
