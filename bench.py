@@ -1,25 +1,29 @@
 #!/usr/bin/env python3
 """bench.py -- grad-codec GB/s (dense fp32 in) per GPU, thresholdv16 k=1% on 64 MiB buckets.
 
-Workload (BASELINE.json metric): one *step* is one batched
-thresholdv16 compress over the 8 gradient buckets of one iteration: 8 keys
-("<layer>@weight") x 64 MiB fp32 (n = 16,777,216, dst_len = 167,772 =
-merge_numel(n, 0.99)), device resident, one C-ABI call
-(stg_codec_compress_batch_device) = one persistent kernel launch.  Each rank
-holds 2 buffer sets (the engine's iter%2 shm buffers, core.cpp:967) = 16
-distinct buckets (1 GiB > 2x the 256 MB Infinity Cache); step s compresses
-set s%2, so every key sees fresh data each visit and its AIMD threshold runs
-its real regime A/B sequence.  Keys are initialised (first-threshold call)
-before the warmup steps.  value = 8 x 64 MiB x steps / time.
+Workload (BASELINE.json metric): one *step* compresses the 16
+gradient buckets of one iteration with thresholdv16: 16 keys ("<layer>@weight")
+x 64 MiB fp32 (n = 16,777,216, dst_len = 167,772 = merge_numel(n, 0.99)),
+device resident.  The engine issues its MERGE-compress tasks from several
+pool workers at once (engine/modules/compress.cpp:141, config.h:7); here the
+step is two batched C-ABI calls (stg_codec_compress_batch_device) of 8
+buckets each on two streams = two concurrent persistent launches, so one
+launch's exchange tail overlaps the other's streaming.  Each rank holds 2
+buffer sets (the engine's iter%2 shm buffers, core.cpp:967) = 32 distinct
+buckets (2 GiB >> the 256 MB Infinity Cache); step s compresses set s%2, so
+every key sees fresh data each visit and its AIMD threshold runs its real
+regime A/B sequence.  Keys are initialised (first-threshold call) before the
+warmup.  value = 16 x 64 MiB x steps / time.
 
 Multi-GPU: buckets are independent, so each rank compresses its
 own buckets with no collective on the data path ("scaling": "weak");
 value = bytes of all ranks / max-over-ranks time.
 
 Extra fields: ``roofline`` for the dominant (only) kernel, tv16_batch, timed
-live with HIP events on the codec's stream (algorithmic bytes per launch =
-8 x (4n + 8k)), ``cpu_baseline`` (the oracle port of backend/src/compress
-timed on this host, rank 0 at N=1 only).
+live with HIP events (algorithmic bytes = 4n + 8k per bucket, over the
+interval that brackets the profiled launches of all streams; the per-launch
+average duration is reported beside it), ``cpu_baseline`` (the oracle port
+of backend/src/compress timed on this host, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
@@ -48,7 +52,8 @@ def parse():
     p.add_argument("--method", default="thresholdv16")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--profile-steps", type=int, default=16)
+    p.add_argument("--profile-steps", type=int, default=64)
+    p.add_argument("--warmup-seconds", type=float, default=2.0)
     p.add_argument("--streams", type=int, default=2,
                    help="issue key i's calls on stream i %% S, like the engine's worker pool; with S > 1 each "
                         "persistent launch takes one workgroup per CU so two launches share the chip")
@@ -163,6 +168,15 @@ def main():
     for s in range(args.warmup):
         step(s + 1)
     sync_streams()
+    # the GPU holds low clocks for a while after going busy: keep stepping
+    # until --warmup-seconds have passed before anything is timed
+    t0 = time.perf_counter()
+    s = args.warmup + 1
+    while time.perf_counter() - t0 < args.warmup_seconds:
+        for _ in range(16):
+            step(s)
+            s += 1
+        sync_streams()
 
     # ---- timed region ----
     if world > 1:
@@ -184,12 +198,30 @@ def main():
     if not os.environ.get("STG_DEBUG_TV16_STAGE"):
         assert int(counts.min().item()) == k
 
-    # ---- live per-launch timing (HIP events on the codec's stream) ----
-    comp.set_timing(True)
+    # ---- live kernel timing (HIP events) ----
+    # per launch: the events the codec records around every tv16_batch launch
+    # on its stream (stg_codec_set_timing); chip level: events on stream 0
+    # bracketing the profile steps of all streams (with S streams, S launches
+    # overlap, so bytes / interval is the chip's rate, and S x interval /
+    # launches is the per-launch duration rocprofv3 reports).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev0.record(stream)
+    for st in streams[1:]:
+        st.wait_event(ev0)
+    for s in range(args.profile_steps):
+        step(s)
+    for st in streams[1:]:
+        stream.wait_stream(st)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    chip_ms = ev0.elapsed_time(ev1)
+    comp.set_timing(True)  # a second pass: per-launch events (they cost a little themselves)
     for s in range(args.profile_steps):
         step(s)
     (kern_ms, _fill_ms, call_ms), launches = comp.get_timing()
     comp.set_timing(False)
+    launches = args.profile_steps * ns  # launches in the chip interval (one per stream and step)
     kern_us = kern_ms * 1e3 / max(launches, 1)
     per_launch = nk // ns
 
@@ -198,7 +230,10 @@ def main():
     value = total_bytes / el / 1e9
     if rank == 0:
         alg = per_launch * (4.0 * n + 8.0 * k)  # 4n + 8k per bucket
-        achieved = alg / (kern_us * 1e-6) / 1e9
+        # algorithmic bytes of every launch in the profiled interval / the
+        # interval (= alg per launch / (avg launch duration / S) when the S
+        # streams' launches overlap fully)
+        achieved = alg * launches / (chip_ms * 1e-3) / 1e9
         out = {
             "metric": "grad-codec GB/s (dense fp32 in) per GPU; thresholdv16 k=1% on 64 MiB bucket",
             "value": round(value, 2),
@@ -211,14 +246,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (splitmix64 Irwin-Hall D1, 2 x 8 distinct 64 MiB buckets per GPU, device resident)",
+            "data": f"synthetic (splitmix64 Irwin-Hall D1, 2 x {nk} distinct {args.mib} MiB buckets per GPU, "
+                    "device resident)",
             "config": {"workload": f"{args.method} k={k} (1%) on {args.mib} MiB fp32 buckets; step = one batched "
                                    f"call over {nk} keys ({nk * args.mib} MiB)",
                        "streams": ns, "buckets_per_launch": per_launch,
                        "n": n, "dst_len": k, "parallelism": f"bucket-sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(per_launch),
-                         "kernel": "tv16_batch", "alg_bytes_per_launch": int(alg), "avg_us": round(kern_us, 2)},
+                         "kernel": "tv16_batch", "alg_bytes_per_launch": int(alg), "avg_us": round(kern_us, 2),
+                         "concurrent_launches": ns, "launches_timed": int(launches),
+                         "interval_us": round(chip_ms * 1e3, 1)},
             "per_bucket_us": round(el * 1e6 / (args.steps * nk), 3),
             "first_call_ms": round(first_ms, 3),
             "host_enqueue_us_per_step": round(t_enq * 1e6 / args.steps, 2),

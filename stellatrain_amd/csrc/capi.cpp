@@ -402,8 +402,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         KeyState *st;
         bool fresh;
         if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
-        const size_t ntiles = (n + stg::TV_TILE - 1) / stg::TV_TILE;
-        if ((rc = ws->ensure(1, ntiles, ntiles * stg::TV_STAGE))) return rc;
+        if ((rc = ws->ensure(1, stg::TV_MAXG, (size_t)stg::TV_MAXG * stg::TV_SCAP))) return rc;
         stg::TvLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, d_count, st, fresh, h->num_cu, ev};
         HIP_TRY(stg::launch_tv(a, ws->d, s));
     } else {

@@ -10,19 +10,31 @@
 // k < cnt -> t = fma(0.01*cnt/k, gmax, t) in double (GCC contracts it at -O3).
 // Returns min(cnt, cap).  The state is keyed by the src pointer (:44).
 //
-// GPU structure: tv_scan streams the bucket (8192-element tiles, one float4
-// per lane per step), stages each tile's qualifiers (in order) in a fixed
-// per-tile slot and records per-tile counts and max|x|; tv_fill (one
-// workgroup per CU) turns tile counts into global offsets, copies the staged
-// pairs to their final place (re-deriving a tile from src in the rare case it
-// overflowed its staging slot) and updates the threshold on the device.
+// GPU structure (two launches, both HBM-bound):
+//   tv_scan  persistent, 1024-thread workgroups (2 per CU), each owning a
+//            contiguous range of the bucket: 16 waves stream it with a rolling
+//            pipeline of SCAN_D nontemporal float4 loads per lane, count the
+//            qualifiers and max|x|, and list the qualifiers (position, value)
+//            in LDS; at the end the list is put in position order (a counting
+//            rank over the list) and written to the workgroup's staging slot.
+//   tv_fill  one workgroup per range: the prefix of the ranges' counts places
+//            the range's sorted list in the output (capped); workgroup 0 folds
+//            the maxima and writes the AIMD threshold and the count.  A range
+//            whose list overflowed its LDS capacity is re-scanned in order.
 #include <algorithm>
 
-#include "tile.h"
+#include "ws.h"
 
 namespace stg {
 
 namespace {
+
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t TWG = 1024;       // threads per workgroup (16 waves)
+constexpr uint32_t TNW = TWG / 64;
+constexpr uint32_t SCAN_D = 4;       // float4 loads in flight per lane
+constexpr uint32_t LCAP = TV_SCAP;   // qualifiers listed in LDS per range
 
 __global__ void tv_init_state(KeyState *st, const RSel *rs) {
     st->t = u2f(rs->prefix);
@@ -30,137 +42,196 @@ __global__ void tv_init_state(KeyState *st, const RSel *rs) {
     st->init = 1;
 }
 
-template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) tv_scan(const float *__restrict__ src, size_t n,
-                                                  const KeyState *__restrict__ state, uint32_t *__restrict__ tile_cnt,
-                                                  uint32_t *__restrict__ tile_max, uint32_t *__restrict__ stage_pos,
-                                                  float *__restrict__ stage_val, CallParams *cp) {
-    __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
-    __shared__ uint32_t s_max[STG_WAVES];
+// Range of workgroup w in float4 units; the ragged n % 4 tail belongs to the
+// last range.
+struct TvRange {
+    uint64_t lo, len;
+};
+__device__ __forceinline__ TvRange tv_range(uint64_t n4, uint32_t G, uint32_t w) {
+    const uint64_t per = n4 / G, rem = n4 % G;
+    TvRange r;
+    r.lo = w * per + std::min<uint64_t>(w, rem);
+    r.len = per + (w < rem ? 1u : 0u);
+    return r;
+}
+
+__global__ void __launch_bounds__(TWG, 8) tv_scan(const float *__restrict__ src, uint64_t n,
+                                                   const KeyState *__restrict__ state, uint32_t *__restrict__ wg_cnt,
+                                                   uint32_t *__restrict__ wg_max, uint32_t *__restrict__ stage_pos,
+                                                   float *__restrict__ stage_val, CallParams *cp) {
+    __shared__ uint32_t s_pos[LCAP];
+    __shared__ float s_val[LCAP];
+    __shared__ uint32_t s_n, s_cnt[TNW], s_max[TNW];
+    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const float t = state->t;
-    if (blockIdx.x == 0 && threadIdx.x == 0) cp->t = t;  // the fill kernel reads t from here
-    const size_t base = (size_t)blockIdx.x * TV_TILE;
-    float4 v[TILE_U];
-    load_tile<VEC>(src, n, base, 0xffffffffu, v);
-    uint32_t q = 0, mx = 0;
+    if (w == 0 && tid == 0) cp->t = t;  // the fill kernel reads t from here
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    const uint64_t n4 = n / 4;
+    const TvRange R = tv_range(n4, G, w);
+    // the range as a bounded buffer: lanes past it read zeros (launch_tv keeps
+    // every range below 2^28 float4)
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(src + R.lo * 4), 0, (uint32_t)(R.len * 16), 0x00020000);
+    const uint32_t steps = (uint32_t)((R.len + 63) / 64);  // 64 float4 per wave step
+    const uint32_t mine = steps > wave ? (steps - wave + TNW - 1) / TNW : 0u;
+    auto load = [&](uint32_t m) -> float4 {
+        uint32_t voff = (wave * 64 + lane) * 16u;
+        asm volatile("" : "+v"(voff));
+        const u4v q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + m * (TNW * 1024u), 0, 2 /* nt */);
+        return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
+    };
+    uint32_t cnt = 0, mx = 0;
+    float4 v[SCAN_D];
 #pragma unroll
-    for (uint32_t u = 0; u < TILE_U; ++u) {
-        const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
+    for (uint32_t u = 0; u < SCAN_D; ++u) v[u] = load(u);
+    for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float x = comp(v[u], j);
-            const bool valid = e + j < n;
-            const float ax = fabsf(x);
-            if (valid) mx = max(mx, f2u(ax));
-            if (valid && ax >= t) q |= 1u << (u * 4 + j);
-        }
-    }
-    uint32_t slot[TILE_U * 4], total;
-    tile_ranks(q, slot, s_wt, &total);
-    if (q) {
+        for (uint32_t u = 0; u < SCAN_D; ++u) {
+            const float4 x = v[u];
+            v[u] = load(m0 + u + SCAN_D);
+            const uint32_t f = ((m0 + u) * TNW + wave) * 64 + lane;  // float4 within the range
+            const bool in = f < R.len;
+            const float a0 = fabsf(x.x), a1 = fabsf(x.y), a2 = fabsf(x.z), a3 = fabsf(x.w);
+            if (in) mx = max(mx, max(max(f2u(a0), f2u(a1)), max(f2u(a2), f2u(a3))));
+            const uint32_t q = in ? ((uint32_t)(a0 >= t) | ((uint32_t)(a1 >= t) << 1) | ((uint32_t)(a2 >= t) << 2) |
+                                     ((uint32_t)(a3 >= t) << 3))
+                                  : 0u;
+            if (__ballot(q != 0) && q) {  // rare: list this lane's qualifiers
+                const uint32_t c = (uint32_t)__popc(q);
+                cnt += c;
+                uint32_t o = atomicAdd(&s_n, c);
+                const uint32_t p0 = (uint32_t)((R.lo + f) * 4);
+                const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-        for (uint32_t u = 0; u < TILE_U; ++u) {
-            const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (((q >> (u * 4 + j)) & 1u) && slot[u * 4 + j] < TV_STAGE) {
-                    const size_t o = (size_t)blockIdx.x * TV_STAGE + slot[u * 4 + j];
-                    stage_pos[o] = (uint32_t)(e + j);
-                    stage_val[o] = comp(v[u], j);
+                for (uint32_t j = 0; j < 4; ++j) {
+                    if ((q >> j) & 1u) {
+                        if (o < LCAP) { s_pos[o] = p0 + j; s_val[o] = xs[j]; }
+                        ++o;
+                    }
                 }
             }
         }
     }
+    // the ragged tail (n % 4 elements) closes the last range
+    if (w == G - 1 && tid == 0) {
+        for (uint64_t e = n4 * 4; e < n; ++e) {
+            const float x = src[e], a = fabsf(x);
+            mx = max(mx, f2u(a));
+            if (a >= t) {
+                const uint32_t o = atomicAdd(&s_n, 1u);
+                ++cnt;
+                if (o < LCAP) { s_pos[o] = (uint32_t)e; s_val[o] = x; }
+            }
+        }
+    }
+    cnt = wave_sum(cnt);
     mx = wave_max(mx);
-    if (__lane_id() == 0) s_max[threadIdx.x >> 6] = mx;
+    if (lane == 0) { s_cnt[wave] = cnt; s_max[wave] = mx; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = 0;
-        for (uint32_t w = 0; w < STG_WAVES; ++w) m = max(m, s_max[w]);
-        tile_cnt[blockIdx.x] = total;
-        tile_max[blockIdx.x] = m;
+    const uint32_t listed = s_n;
+    if (tid == 0) {
+        uint32_t c = 0, m = 0;
+        for (uint32_t i = 0; i < TNW; ++i) { c += s_cnt[i]; m = max(m, s_max[i]); }
+        wg_cnt[w] = c;
+        wg_max[w] = m;
+    }
+    // position order: rank = listed entries with a smaller position
+    if (listed <= LCAP) {
+        for (uint32_t e = tid; e < listed; e += TWG) {
+            const uint32_t p = s_pos[e];
+            uint32_t r = 0;
+            for (uint32_t x = 0; x < listed; ++x) r += s_pos[x] < p;
+            stage_pos[(size_t)w * LCAP + r] = p;
+            stage_val[(size_t)w * LCAP + r] = s_val[e];
+        }
     }
 }
 
 struct TvFillArgs {
     const float *src;
     uint64_t n;
-    uint32_t ntiles, k, cap;
+    uint32_t k, cap;
     uint32_t *idx;
     float *val;
     uint32_t *count_out;
     KeyState *state;
     const CallParams *cp;
-    const uint32_t *tile_cnt;
-    const uint32_t *tile_max;
+    const uint32_t *wg_cnt;
+    const uint32_t *wg_max;
     const uint32_t *stage_pos;
     const float *stage_val;
 };
 
-template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) tv_fill(TvFillArgs a) {
-    __shared__ uint64_t sh64[STG_WAVES];
-    __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
-    __shared__ uint32_t s_max[STG_WAVES];
+__global__ void __launch_bounds__(TWG) tv_fill(TvFillArgs a) {
+    __shared__ uint64_t sh64[TNW];
+    __shared__ uint32_t s_mx[TNW];
+    __shared__ uint32_t sh[TNW + 1];
     const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    const uint32_t t_begin = (uint32_t)((uint64_t)w * a.ntiles / G);
-    const uint32_t t_end = (uint32_t)((uint64_t)(w + 1) * a.ntiles / G);
     const float t = a.cp->t;  // the state slot itself is rewritten by workgroup 0 below
-
     uint64_t tot = 0, bef = 0;
     uint32_t mx = 0;
-    for (uint32_t i = tid; i < a.ntiles; i += STG_WG) {
-        const uint32_t c = a.tile_cnt[i];
+    for (uint32_t i = tid; i < G; i += TWG) {
+        const uint32_t c = a.wg_cnt[i];
         tot += c;
-        if (i < t_begin) bef += c;
-        if (w == 0) mx = max(mx, a.tile_max[i]);
+        if (i < w) bef += c;
+        mx = max(mx, a.wg_max[i]);
     }
-    const uint64_t cnt = wg_sum64(tot, sh64);
-    uint64_t P = wg_sum64(bef, sh64);
-
-    for (uint32_t tile = t_begin; tile < t_end && P < a.cap; ++tile) {
-        const uint32_t c = a.tile_cnt[tile];
+    const uint64_t cnt = blk_sum64<TNW>(tot, sh64);
+    const uint64_t P = blk_sum64<TNW>(bef, sh64);
+    const uint32_t c = a.wg_cnt[w];
+    if (P < a.cap && c) {
         const uint32_t m = (uint32_t)std::min<uint64_t>(c, a.cap - P);
-        if (c <= TV_STAGE) {
-            for (uint32_t i = tid; i < m; i += STG_WG) {
-                a.idx[P + i] = a.stage_pos[(size_t)tile * TV_STAGE + i];
-                a.val[P + i] = a.stage_val[(size_t)tile * TV_STAGE + i];
+        if (c <= LCAP) {
+            for (uint32_t i = tid; i < m; i += TWG) {
+                a.idx[P + i] = a.stage_pos[(size_t)w * LCAP + i];
+                a.val[P + i] = a.stage_val[(size_t)w * LCAP + i];
             }
-        } else {  // staging overflowed: re-derive this tile's ranks from src
-            float4 v[TILE_U];
-            const size_t base = (size_t)tile * TV_TILE;
-            load_tile<VEC>(a.src, a.n, base, 0xffffffffu, v);
-            uint32_t q = 0;
+        } else {
+            // the range's list overflowed: its qualifiers again, in order
+            const uint64_t n4 = a.n / 4;
+            const TvRange R = tv_range(n4, G, w);
+            const uint64_t units = R.len + (w == G - 1 && a.n % 4 ? 1u : 0u);  // + the ragged tail
+            uint64_t base = 0;
+            for (uint64_t f0 = 0; f0 < units && base < m; f0 += TWG) {
+                const uint64_t f = f0 + tid;
+                uint32_t q = 0;
+                float xs[4] = {0.f, 0.f, 0.f, 0.f};
+                if (f < units) {
 #pragma unroll
-            for (uint32_t u = 0; u < TILE_U; ++u) {
-                const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (e + j < a.n && fabsf(comp(v[u], j)) >= t) q |= 1u << (u * 4 + j);
-            }
-            uint32_t slot[TILE_U * 4], total;
-            tile_ranks(q, slot, s_wt, &total);
-#pragma unroll
-            for (uint32_t u = 0; u < TILE_U; ++u) {
-                const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (((q >> (u * 4 + j)) & 1u) && slot[u * 4 + j] < m) {
-                        a.idx[P + slot[u * 4 + j]] = (uint32_t)(e + j);
-                        a.val[P + slot[u * 4 + j]] = comp(v[u], j);
+                    for (uint32_t j = 0; j < 4; ++j) {
+                        const uint64_t e = (R.lo + f) * 4 + j;
+                        if (e < a.n) {
+                            xs[j] = a.src[e];
+                            q |= (uint32_t)(fabsf(xs[j]) >= t) << j;
+                        }
                     }
+                }
+                uint32_t total;
+                const uint32_t ex = blk_excl_scan<TNW>((uint32_t)__popc(q), sh, &total);
+                uint64_t o = base + ex;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    if ((q >> j) & 1u) {
+                        if (o < m) {
+                            a.idx[P + o] = (uint32_t)((R.lo + f) * 4 + j);
+                            a.val[P + o] = xs[j];
+                        }
+                        ++o;
+                    }
+                }
+                base += total;
             }
         }
-        P += c;
     }
-
     if (w == 0) {
         mx = wave_max(mx);
-        if (__lane_id() == 0) s_max[tid >> 6] = mx;
+        if ((tid & 63) == 0) s_mx[tid >> 6] = mx;
         __syncthreads();
         if (tid == 0) {
             uint32_t g = 0;
-            for (uint32_t i = 0; i < STG_WAVES; ++i) g = max(g, s_max[i]);
+            for (uint32_t i = 0; i < TNW; ++i) g = max(g, s_mx[i]);
             const float gmax = a.n ? u2f(g) : -1.f;
             float nt = t;
             if ((uint64_t)a.k > cnt) nt = (float)((double)t * 0.99);
@@ -175,21 +246,22 @@ __global__ void __launch_bounds__(STG_WG) tv_fill(TvFillArgs a) {
 }  // namespace
 
 hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
-    const uint32_t ntiles = (uint32_t)((a.n + TV_TILE - 1) / TV_TILE);
     if (a.first) {
         const uint32_t rank = (uint32_t)std::min<uint64_t>(a.k, a.n - 1);
         hipError_t e = launch_radix_select(a.src, a.n, 0xffffffffu, 0, nullptr, rank, ws, a.num_cu, s);
         if (e != hipSuccess) return e;
         tv_init_state<<<1, 1, 0, s>>>(a.state, ws.rsel);
     }
+    // 2 workgroups per CU, each with >= 64 KiB of the bucket
+    const uint64_t n4 = a.n / 4;
+    const uint32_t G = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(std::min<uint64_t>(2u * (uint64_t)a.num_cu, TV_MAXG), (n4 + 4095) / 4096));
+    if (n4 / G + 1 >= (1ull << 28)) return hipErrorInvalidValue;  // a range must fit one buffer descriptor
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    const bool vec = (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0;
-    if (vec) tv_scan<true><<<ntiles, STG_WG, 0, s>>>(a.src, a.n, a.state, ws.tile_cnt, ws.tile_aux, ws.stage_pos, ws.stage_val, ws.cp);
-    else tv_scan<false><<<ntiles, STG_WG, 0, s>>>(a.src, a.n, a.state, ws.tile_cnt, ws.tile_aux, ws.stage_pos, ws.stage_val, ws.cp);
+    tv_scan<<<G, TWG, 0, s>>>(a.src, a.n, a.state, ws.tile_cnt, ws.tile_aux, ws.stage_pos, ws.stage_val, ws.cp);
     TvFillArgs f;
     f.src = a.src;
     f.n = a.n;
-    f.ntiles = ntiles;
     f.k = a.k;
     f.cap = a.cap;
     f.idx = a.idx;
@@ -197,14 +269,12 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     f.count_out = a.count_out;
     f.state = a.state;
     f.cp = ws.cp;
-    f.tile_cnt = ws.tile_cnt;
-    f.tile_max = ws.tile_aux;
+    f.wg_cnt = ws.tile_cnt;
+    f.wg_max = ws.tile_aux;
     f.stage_pos = ws.stage_pos;
     f.stage_val = ws.stage_val;
-    const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)a.num_cu, ntiles));
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    if (vec) tv_fill<true><<<G, STG_WG, 0, s>>>(f);
-    else tv_fill<false><<<G, STG_WG, 0, s>>>(f);
+    tv_fill<<<G, TWG, 0, s>>>(f);
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
     return hipGetLastError();
 }

@@ -875,7 +875,11 @@ __device__ __forceinline__ void rank_window(Ctx &C, uint32_t r, uint32_t R, cons
 
 // Rare paths: the window does not hold the top M -> radix descent over the
 // bucket's line sums (ranker w takes chunks w, w + G, ...; sums recomputed
-// from src into sums_g) with grid barriers among the rankers, then rank and emit.
+// from src into sums_g) with grid barriers among the rankers, then rank and
+// emit.  The top M lines are taken in pieces of at most CAND_CAP - 1
+// candidates (the LDS rank capacity), in output order: each piece is the
+// next run of keys below the previous piece's cut, so a large M (the count
+// fell far short of k) is emitted piece by piece at increasing offsets.
 __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, uint32_t cnt, uint32_t M, float t,
                                           float tail_key) {
     const BucketDesc &d = C.A.bk[b];
@@ -883,7 +887,6 @@ __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, ui
     const uint32_t G = C.G, w = C.w, lane = flane();
     const bool vec = aligned16(d);
     const uint32_t tb = f2u(t);
-    const bool tail_cand = (flags & DEC_TAIL) != 0;
     uint64_t *cand = C.cand(b);
     BucketCtl *bc = &C.cc()->bk[b];
     // this ranker's lines: chunks c = w, w + G, ... of the bucket
@@ -899,177 +902,216 @@ __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, ui
     });
     vm_drain();
     auto get_sum = [&](uint32_t li) -> float { return d.sums_g[li]; };
-    const uint32_t hi0 = tb - 1u;  // largest candidate key (keys u < tb)
-    uint32_t mode = 1, blo = tb, ustar = 0, greater = 0;
-    if (M > 0) {
-        for (uint32_t i = lane; i < HBINS; i += 64) L.hist[i] = 0;
-        lds_drain();
-        for_lines([&](uint32_t li, bool ok, uint32_t) {
-            if (!ok) return;
-            const uint32_t u = f2u(get_sum(li));
-            if (u < tb) atomicAdd(&L.hist[std::min((hi0 - u) >> L1_SHIFT, HBINS - 1)], 1u);
-        });
-        lds_drain();
-        for (uint32_t i = lane; i < HBINS; i += 64) {
-            const uint32_t h = L.hist[i];
-            if (h) g_add(&bc->hist[0][i], h);
-        }
-        C.grid_sync();
-        uint32_t lvl = 0, hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
-        bool ovf = true;
-        constexpr uint32_t BPL = HBINS / 64;  // bins per lane
-        for (;;) {
-            // locate the bin holding rank `need` (1-based) counting down from hi
-            const uint32_t need = M - above;
-            uint32_t loc = 0;
-            for (uint32_t jj = 0; jj < BPL; ++jj) loc += ld_acq_relaxed(&bc->hist[lvl][lane * BPL + jj]);
-            const uint32_t incl = wave_incl_scan(loc);
-            const uint32_t excl = incl - loc;
-            const uint64_t fm = __ballot(need > excl && need <= incl);
-            uint32_t bstar = 0xffffffffu, cum = 0, hb = 0;
-            if (fm) {
-                const uint32_t src_lane = (uint32_t)__ffsll((long long)fm) - 1u;
-                if (lane == src_lane) {
-                    uint32_t cc = excl;
-                    for (uint32_t jj = 0; jj < BPL; ++jj) {
-                        const uint32_t h = ld_acq_relaxed(&bc->hist[lvl][lane * BPL + jj]);
-                        if (need <= cc + h) { bstar = lane * BPL + jj; cum = cc; hb = h; break; }
-                        cc += h;
-                    }
-                }
-                bstar = (uint32_t)__builtin_amdgcn_readlane((int)bstar, (int)src_lane);
-                cum = (uint32_t)__builtin_amdgcn_readlane((int)cum, (int)src_lane);
-                hb = (uint32_t)__builtin_amdgcn_readlane((int)hb, (int)src_lane);
-            }
-            if (bstar == 0xffffffffu) {  // histogram does not reach `need`: collect all
-                if (lane == 0) C.fail(FAIL_LEVELS);
-                mode = 1; blo = 0;
-                break;
-            }
-            if (ovf && bstar == HBINS - 1) {
-                above += cum;
-                const uint64_t width = (uint64_t)(HBINS - 1) << s;
-                if ((uint64_t)hi < width) {
-                    if (lane == 0) C.fail(FAIL_LEVELS);
-                    mode = 1; blo = 0;
-                    break;
-                }
-                hi = hi - (uint32_t)width;
-                lo = 0;
-                s = bitlen(hi) > 10 ? bitlen(hi) - 10 : 0;
-                ovf = false;
-            } else {
-                const uint32_t bhi = hi - (bstar << s);
-                const int64_t blo64 = (int64_t)hi - ((int64_t)(bstar + 1) << s) + 1;
-                const uint32_t bl = (uint32_t)std::max<int64_t>((int64_t)lo, blo64);
-                const uint32_t totc = above + cum + hb;
-                if (totc + 1 <= CAND_CAP) { mode = 1; blo = bl; break; }
-                if (s == 0) { mode = 2; ustar = bhi; greater = above + cum; break; }
-                above += cum;
-                hi = bhi;
-                lo = bl;
-                s = s >= 10 ? s - 10 : 0;
-            }
-            if (++lvl >= MAX_LEVELS) {
-                if (lane == 0) C.fail(FAIL_LEVELS);
-                mode = 1; blo = lo;
-                break;
-            }
+    const uint32_t tailpos = d.nb * 16;
+    const uint32_t ut = f2u(tail_key);
+    bool tail_left = (flags & DEC_TAIL) != 0;  // the ragged tail competes and is not yet emitted
+    uint32_t ub = tb;                          // keys u < ub are not yet emitted
+    uint32_t left = M;                         // full lines still to emit
+    uint32_t eoff = cnt;                       // output offset of the next piece
+    for (uint32_t piece = 0;; ++piece) {
+        // a later piece reuses the level histograms (zeroed by the previous
+        // piece after its last read), the candidate buffer and the tie counts
+        if (piece) C.grid_sync();
+        const uint32_t nbase = uni(ld_acq_relaxed(&bc->cand_n));
+        const uint32_t need = std::min(left, CAND_CAP - 1u);
+        const uint32_t hi0 = ub ? ub - 1u : 0u;  // largest remaining key
+        uint32_t mode = 1, blo = ub, ustar = 0, greater = 0, ties_n = 0, lvl = 0;
+        bool final = true;
+        if (need > 0 && ub > 0) {
             for (uint32_t i = lane; i < HBINS; i += 64) L.hist[i] = 0;
             lds_drain();
             for_lines([&](uint32_t li, bool ok, uint32_t) {
                 if (!ok) return;
                 const uint32_t u = f2u(get_sum(li));
-                if (u < tb && u >= lo && u <= hi) atomicAdd(&L.hist[(hi - u) >> s], 1u);
+                if (u < ub) atomicAdd(&L.hist[std::min((hi0 - u) >> L1_SHIFT, HBINS - 1)], 1u);
             });
             lds_drain();
             for (uint32_t i = lane; i < HBINS; i += 64) {
                 const uint32_t h = L.hist[i];
-                if (h) g_add(&bc->hist[lvl][i], h);
+                if (h) g_add(&bc->hist[0][i], h);
             }
             C.grid_sync();
+            uint32_t hi = hi0, lo = 0, s = L1_SHIFT, above = 0;
+            bool ovf = true;
+            constexpr uint32_t BPL = HBINS / 64;  // bins per lane
+            for (;;) {
+                // locate the bin holding rank `need - above` (1-based) counting down from hi
+                const uint32_t want = need - above;
+                uint32_t loc = 0;
+                for (uint32_t jj = 0; jj < BPL; ++jj) loc += ld_acq_relaxed(&bc->hist[lvl][lane * BPL + jj]);
+                const uint32_t incl = wave_incl_scan(loc);
+                const uint32_t excl = incl - loc;
+                const uint64_t fm = __ballot(want > excl && want <= incl);
+                uint32_t bstar = 0xffffffffu, cum = 0, hb = 0;
+                if (fm) {
+                    const uint32_t src_lane = (uint32_t)__ffsll((long long)fm) - 1u;
+                    if (lane == src_lane) {
+                        uint32_t cc = excl;
+                        for (uint32_t jj = 0; jj < BPL; ++jj) {
+                            const uint32_t h = ld_acq_relaxed(&bc->hist[lvl][lane * BPL + jj]);
+                            if (want <= cc + h) { bstar = lane * BPL + jj; cum = cc; hb = h; break; }
+                            cc += h;
+                        }
+                    }
+                    bstar = (uint32_t)__builtin_amdgcn_readlane((int)bstar, (int)src_lane);
+                    cum = (uint32_t)__builtin_amdgcn_readlane((int)cum, (int)src_lane);
+                    hb = (uint32_t)__builtin_amdgcn_readlane((int)hb, (int)src_lane);
+                }
+                if (bstar == 0xffffffffu) {  // histogram does not reach `need`: collect all
+                    if (lane == 0) C.fail(FAIL_LEVELS);
+                    mode = 1; blo = 0;
+                    break;
+                }
+                if (ovf && bstar == HBINS - 1) {
+                    above += cum;
+                    const uint64_t width = (uint64_t)(HBINS - 1) << s;
+                    if ((uint64_t)hi < width) {
+                        if (lane == 0) C.fail(FAIL_LEVELS);
+                        mode = 1; blo = 0;
+                        break;
+                    }
+                    hi = hi - (uint32_t)width;
+                    lo = 0;
+                    s = bitlen(hi) > 10 ? bitlen(hi) - 10 : 0;
+                    ovf = false;
+                } else {
+                    const uint32_t bhi = hi - (bstar << s);
+                    const int64_t blo64 = (int64_t)hi - ((int64_t)(bstar + 1) << s) + 1;
+                    const uint32_t bl = (uint32_t)std::max<int64_t>((int64_t)lo, blo64);
+                    const uint32_t totc = above + cum + hb;
+                    // keys in [bl, ub): the whole piece fits the rank capacity
+                    if (totc + 1 <= CAND_CAP) { mode = 1; blo = bl; final = need == left; break; }
+                    // one key value: the keys above it, then its ties in position order
+                    if (s == 0) {
+                        mode = 2; ustar = bhi; greater = above + cum; ties_n = hb;
+                        final = greater + ties_n >= left;
+                        break;
+                    }
+                    above += cum;
+                    hi = bhi;
+                    lo = bl;
+                    s = s >= 10 ? s - 10 : 0;
+                }
+                if (lvl + 1 >= MAX_LEVELS) {
+                    if (lane == 0) C.fail(FAIL_LEVELS);
+                    mode = 1; blo = lo;
+                    break;
+                }
+                ++lvl;
+                for (uint32_t i = lane; i < HBINS; i += 64) L.hist[i] = 0;
+                lds_drain();
+                for_lines([&](uint32_t li, bool ok, uint32_t) {
+                    if (!ok) return;
+                    const uint32_t u = f2u(get_sum(li));
+                    if (u < ub && u >= lo && u <= hi) atomicAdd(&L.hist[(hi - u) >> s], 1u);
+                });
+                lds_drain();
+                for (uint32_t i = lane; i < HBINS; i += 64) {
+                    const uint32_t h = L.hist[i];
+                    if (h) g_add(&bc->hist[lvl][i], h);
+                }
+                C.grid_sync();
+            }
         }
-    }
 
-    const uint32_t tailpos = d.nb * 16;
-    const bool tail_in_greater = tail_cand && mode == 2 && tail_key > u2f(ustar);
-    // collect: mode 1 -> keys in [blo, tb); mode 2 -> keys in (ustar, tb);
-    // one slot range per ranker; mode 2 also counts each chunk's ties at ustar
-    if (M > 0) {
-        const uint32_t kmin = mode == 1 ? blo : ustar + 1;
-        uint32_t mine = 0;
-        for_lines([&](uint32_t li, bool ok, uint32_t) {
-            if (!ok) return;
-            const uint32_t u = f2u(get_sum(li));
-            mine += u < tb && u >= kmin;
-        });
-        mine = uni(wave_sum(mine));
-        uint32_t o = 0;
-        if (lane == 0 && mine) o = g_add(&bc->cand_n, mine);
-        uint32_t base = uni(o);
-        for (uint32_t c = w; c < d.nc; c += G) {
-            const uint32_t L0 = c * TV16_CHUNK;
-            const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
-            uint32_t ties = 0;
-            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                uint32_t u = 0;
-                bool p = false;
-                if (i < nl) {
-                    u = f2u(get_sum(L0 + i));
-                    p = u < tb && u >= kmin;
-                    ties += mode == 2 && u == ustar;
-                }
-                const uint64_t m = __ballot(p);
-                const uint32_t ex = (uint32_t)__popcll(m & below_mask(lane));
-                if (p && base + ex < CAND_CAP) st_sc1(&cand[base + ex], cand_key(u, (L0 + i) * 16));
-                base += (uint32_t)__popcll(m);
-            }
-            if (mode == 2) {
-                const uint32_t ct = uni(wave_sum(ties));
-                if (lane == 0) st_sc1(&C.A.desc[d.cs + c].ties, ((uint64_t)C.tag(TAG_TIE) << 32) | ct);
-            }
-        }
-    }
-    C.grid_sync();  // every append / tie count is visible
-    if (mode == 2) {  // lines tied at ustar, in position order after the greater keys
-        const uint32_t base = cnt + 16u * greater + (tail_in_greater ? d.tl : 0u);
-        uint32_t all_ties = 0;
-        for (uint32_t c = lane; c < d.nc; c += 64) all_ties += (uint32_t)ld_sc1(&C.A.desc[d.cs + c].ties);
-        all_ties = uni(wave_sum(all_ties));
-        for (uint32_t c = w; c < d.nc; c += G) {
-            uint32_t before = 0;
-            for (uint32_t c2 = lane; c2 < c; c2 += 64) before += (uint32_t)ld_sc1(&C.A.desc[d.cs + c2].ties);
-            uint32_t rank = uni(wave_sum(before));
-            const uint32_t L0 = c * TV16_CHUNK;
-            const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
-            for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                const bool p = i < nl && f2u(get_sum(L0 + i)) == ustar;
-                const uint64_t m = __ballot(p);
-                if (p) {
+        // the ragged tail's place in this piece
+        // (a negative tail key has the sign bit: u >= ub, never inside a cut)
+        const bool tail_sorted = mode == 1 ? tail_left && (final || (ut >= blo && ut < ub))
+                                           : tail_left && ut > ustar && ut < ub;
+        const bool tail_tie = mode == 2 && tail_left && ut == ustar;
+        // collect: mode 1 -> keys in [blo, ub); mode 2 -> keys in (ustar, ub);
+        // one slot range per ranker; mode 2 also counts each chunk's ties at ustar
+        if (need > 0 && ub > 0) {
+            const uint32_t kmin = mode == 1 ? blo : ustar + 1;
+            uint32_t mine = 0;
+            for_lines([&](uint32_t li, bool ok, uint32_t) {
+                if (!ok) return;
+                const uint32_t u = f2u(get_sum(li));
+                mine += u < ub && u >= kmin;
+            });
+            mine = uni(wave_sum(mine));
+            uint32_t o = nbase;
+            if (lane == 0 && mine) o = g_add(&bc->cand_n, mine);
+            uint32_t base = uni(o) - nbase;
+            for (uint32_t c = w; c < d.nc; c += G) {
+                const uint32_t L0 = c * TV16_CHUNK;
+                const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+                uint32_t ties = 0;
+                for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+                    const uint32_t i = i0 + lane;
+                    uint32_t u = 0;
+                    bool p = false;
+                    if (i < nl) {
+                        u = f2u(get_sum(L0 + i));
+                        p = u < ub && u >= kmin;
+                        ties += mode == 2 && u == ustar;
+                    }
+                    const uint64_t m = __ballot(p);
                     const uint32_t ex = (uint32_t)__popcll(m & below_mask(lane));
-                    const uint64_t off = (uint64_t)base + 16ull * (rank + ex);
-                    if (off < d.dst_len)
-                        emit_line(d, vec, (L0 + i) * 16, (uint32_t)off,
-                                  std::min<uint32_t>(16u, d.dst_len - (uint32_t)off));
+                    if (p && base + ex < CAND_CAP) st_sc1(&cand[base + ex], cand_key(u, (L0 + i) * 16));
+                    base += (uint32_t)__popcll(m);
                 }
-                rank += (uint32_t)__popcll(m);
+                if (mode == 2) {
+                    const uint32_t ct = uni(wave_sum(ties));
+                    if (lane == 0) st_sc1(&C.A.desc[d.cs + c].ties, ((uint64_t)C.tag(TAG_TIE) << 32) | ct);
+                }
             }
         }
-        if (w == 0 && lane == 0 && tail_cand && tail_key == u2f(ustar)) {
-            const uint64_t off = (uint64_t)base + 16ull * all_ties;
-            if (off < d.dst_len)
-                emit_line(d, false, tailpos, (uint32_t)off, std::min<uint32_t>(d.tl, d.dst_len - (uint32_t)off));
+        C.grid_sync();  // every append / tie count is visible; every histogram read is done
+        if (mode == 2) {  // lines tied at ustar, in position order after the greater keys
+            const uint32_t base = eoff + 16u * greater + (tail_sorted ? d.tl : 0u);
+            uint32_t all_ties = 0;
+            for (uint32_t c = lane; c < d.nc; c += 64) all_ties += (uint32_t)ld_sc1(&C.A.desc[d.cs + c].ties);
+            all_ties = uni(wave_sum(all_ties));
+            for (uint32_t c = w; c < d.nc; c += G) {
+                uint32_t before = 0;
+                for (uint32_t c2 = lane; c2 < c; c2 += 64) before += (uint32_t)ld_sc1(&C.A.desc[d.cs + c2].ties);
+                uint32_t rank = uni(wave_sum(before));
+                const uint32_t L0 = c * TV16_CHUNK;
+                const uint32_t nl = d.nb > L0 ? std::min(TV16_CHUNK, d.nb - L0) : 0u;
+                for (uint32_t i0 = 0; i0 < nl; i0 += 64) {
+                    const uint32_t i = i0 + lane;
+                    const bool p = i < nl && f2u(get_sum(L0 + i)) == ustar;
+                    const uint64_t m = __ballot(p);
+                    if (p) {
+                        const uint32_t ex = (uint32_t)__popcll(m & below_mask(lane));
+                        const uint64_t off = (uint64_t)base + 16ull * (rank + ex);
+                        if (off < d.dst_len)
+                            emit_line(d, vec, (L0 + i) * 16, (uint32_t)off,
+                                      std::min<uint32_t>(16u, d.dst_len - (uint32_t)off));
+                    }
+                    rank += (uint32_t)__popcll(m);
+                }
+            }
+            if (w == 0 && lane == 0 && tail_tie) {
+                const uint64_t off = (uint64_t)base + 16ull * all_ties;
+                if (off < d.dst_len)
+                    emit_line(d, false, tailpos, (uint32_t)off, std::min<uint32_t>(d.tl, d.dst_len - (uint32_t)off));
+            }
         }
+        uint32_t nc_all = uni(ld_acq_relaxed(&bc->cand_n)) - nbase;
+        if (nc_all > CAND_CAP) {
+            if (w == 0 && lane == 0) C.fail(FAIL_CAND_OVERFLOW);
+            nc_all = CAND_CAP;
+        }
+        rank_emit(C, C.w, C.G, d, cand, eoff, nc_all, tail_sorted && nc_all < CAND_CAP, tail_key);
+        if (final) break;
+        // next piece: the keys below this one's cut, after its entries
+        const uint32_t lines = mode == 1 ? nc_all : greater + ties_n;
+        const bool tail_out = tail_sorted || tail_tie;
+        eoff += 16u * lines + (tail_out ? d.tl : 0u);
+        left -= std::min(left, lines);
+        if (tail_out) tail_left = false;
+        ub = mode == 1 ? blo : ustar;
+        {  // zero this piece's level histograms (every ranker's reads are done)
+            uint32_t *z = &bc->hist[0][0];
+            const uint32_t words = (lvl + 1) * HBINS;
+            const uint32_t per = (words + G - 1) / G;
+            const uint32_t z0 = w * per, z1 = std::min(words, z0 + per);
+            for (uint32_t i = z0 + lane; i < z1; i += 64) st_sc1(z + i, 0u);
+        }
+        if (eoff >= d.dst_len || left == 0) break;
     }
-    uint32_t nc_all = uni(ld_acq_relaxed(&bc->cand_n));
-    if (nc_all > CAND_CAP) {
-        if (w == 0 && lane == 0) C.fail(FAIL_CAND_OVERFLOW);
-        nc_all = CAND_CAP;
-    }
-    const bool add_tail = mode == 1 ? tail_cand : tail_in_greater;
-    rank_emit(C, C.w, C.G, d, cand, cnt, nc_all, add_tail && nc_all < CAND_CAP, tail_key);
 }
 
 // The heap fill of bucket b, run by every ranker once the bucket's decision

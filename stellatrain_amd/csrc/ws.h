@@ -16,8 +16,9 @@ constexpr uint32_t CAND_CAP = 4096;          // regime-B candidates ranked in LD
 constexpr uint32_t SORT_CAP = 16 * CAND_CAP; // global candidate buffers: one per bucket of a launch
 constexpr uint32_t MAX_FILL_WG = 1024;       // upper bound on fill-kernel workgroups
 
-constexpr uint32_t TV_TILE = 8192;           // threshold-v elements per tile (32 KiB)
-constexpr uint32_t TV_STAGE = 512;           // staged qualifiers per threshold-v tile
+constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)
+constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
+constexpr uint32_t TV_SCAP = 2048;           // threshold-v qualifiers listed per range
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 

@@ -302,3 +302,43 @@ def test_thresholdv16_batch_64mib(gpu, oracle):
     comp.check_device()
     oracle.tv16_free(ho)
     assert regimes  # at least one steady-state call compared
+
+
+@pytest.mark.parametrize("n,k,dist,param", [((1 << 21) + 5, 209715, D1, 0), (1 << 20, 1 << 17, D3, 9000)])
+def test_thresholdv16_large_fill(gpu, oracle, n, k, dist, param):
+    """Regime B with far more lines to fill than one rank piece holds
+    (CAND_CAP - 1 = 4095): the inputs' scale drops 100x between calls, so the
+    ordered scan finds almost nothing above the threshold and the heap fill
+    emits up to k/16 lines in several pieces.  D3 adds exact-zero ties that
+    reach past the pieces."""
+    import torch
+    from parity import canonical_heap_order
+    from stellatrain_amd import ThresholdvCompressor16
+    comp = ThresholdvCompressor16()
+    ho = oracle.tv16_new()
+    big = 0
+    for it, scale in enumerate([1.0, 1.0, 0.01, 1.0, 0.3, 0.003, 0.003]):
+        src = (synth(n, seed_for(11, it), dist, param) * np.float32(scale)).astype(np.float32)
+        t_before = oracle.tv16_state(ho, "f")
+        co, io, vo = oracle.tv16_compress(ho, "f", src, k)
+        idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+        val = torch.zeros(k, dtype=torch.float32, device=gpu)
+        assert comp.compress("f", torch.from_numpy(src).to(gpu), k, idx, val) == co
+        ig, vg = idx.cpu().numpy().view(np.uint32), val.cpu().numpy()
+        so, sg = oracle.tv16_state(ho, "f"), comp.state("f")
+        assert bits(np.array(so, np.float32)).tolist() == bits(np.array(sg, np.float32)).tolist(), it
+        head = _regime_split(oracle, src, k, t_before[0], co) if t_before is not None else 0
+        if t_before is not None and (co - head) // 16 > 4095:
+            big += 1
+        assert_same_stream(ig, vg, io, vo, head)
+        if dist == D3:  # which zero-sum lines fill the tail: position vs heap order
+            np.testing.assert_array_equal(np.sort(bits(vg[:co])), np.sort(bits(vo[:co])))
+            assert np.all(vg[:co] == src[ig[:co]])
+            assert len(np.unique(ig[:co])) == co
+        else:
+            a_i, a_v = canonical_heap_order(ig, vg, head, co, src, oracle)
+            b_i, b_v = canonical_heap_order(io, vo, head, co, src, oracle)
+            assert_same_stream(a_i, a_v, b_i, b_v, co)
+    comp.check_device()
+    oracle.tv16_free(ho)
+    assert big  # at least one call filled more than one piece

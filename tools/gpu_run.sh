@@ -44,6 +44,10 @@ for s in "$@"; do
             unset STG_DEBUG_TV16_STAGE ;;
         ubench) step ubench 300 python tools/ubench_read.py ;;
         configs) step configs 500 python tools/bench_configs.py ;;
+        c2) step c2 300 python tools/bench_configs.py --only c2 ;;
+        c3) step c3 300 python tools/bench_configs.py --only c3 ;;
+        c4) step c4 300 python tools/bench_configs.py --only c4 ;;
+        c5) step c5 300 python tools/bench_configs.py --only c5 ;;
         depths)  # tuning variants built as stellatrain_amd/libstg_codec_d*.so
             for L in stellatrain_amd/libstg_codec_*.so; do
                 v=$(basename $L .so); v=${v#libstg_codec_}
