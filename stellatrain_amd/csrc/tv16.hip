@@ -271,6 +271,12 @@ __device__ __forceinline__ void gather16(const void *src, uint32_t n16, void *ds
     vm_drain();
 }
 
+// Spin-timeout failure bits: FAIL_SPIN_TIMEOUT plus bit 8 + site naming the
+// wait that gave up: 0 grid barrier, 1 buffer set, 2 prefix aggregates,
+// 3 chunk streamed, 4 decision, 5 window lists, 6 / 7 slot chunk id
+// (streamer / finisher), 8 the previous slot's chunk take.
+__device__ __forceinline__ constexpr uint32_t spin_site(uint32_t site) { return FAIL_SPIN_TIMEOUT | (1u << (8 + site)); }
+
 struct Ctx {
     const BatchArgs &A;
     Lds &L;
@@ -314,7 +320,7 @@ struct Ctx {
         }
         for (uint32_t spins = 0; ld_sc1(&fc->slot[w].go) != go; ++spins) {
             __builtin_amdgcn_s_sleep(1);
-            if (spins > SPIN_MAX) { if (lane == 0) fail(FAIL_SPIN_TIMEOUT); break; }
+            if (spins > SPIN_MAX) { if (lane == 0) fail(spin_site(0)); break; }
         }
     }
 };
@@ -336,7 +342,7 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
         uint32_t spins = 0;
         for (; lds_ld(&L.fdone) < j + 1 - NBUF; ++spins) {
             __builtin_amdgcn_s_sleep(2);
-            if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+            if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(1)); break; }
         }
         if (C.stamping && spins && flane() == 0) atomicAdd(&L.stamp[120], spins);
     }
@@ -375,17 +381,23 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     // from the call's counter (slots 0 and 1 are static): late enough that
     // chunks are taken close to when they are streamed (the finishers' prefix
     // counts wait on earlier chunks only), early enough that the round trip
-    // hides behind the second half of the slot.
+    // hides behind the second half of the slot.  A take waits until slot
+    // j - 1's take is published (slot j + 1's chunk id), so a workgroup's
+    // chunk ids increase slot by slot and the first id >= K ends it with no
+    // chunk left behind -- a wave with no steps in a short chunk could
+    // otherwise run ahead into slot j + 1 and take before slot j did.
     uint32_t nx = 0;
     bool grab = false, tried = false;
+    auto try_take = [&]() {
+        tried = true;
+        uint32_t first = 1;
+        if (flane() == 0) first = atomicAdd(&L.mid[j % CIDR], 1u);
+        grab = uni(first) == 0;
+        if (grab && flane() == 0) nx = 2 * C.G + g_add(&C.cc()->next, 1u);
+    };
+    auto prev_taken = [&]() { return lds_ld(&L.cok[(j + 1) % CIDR]) == j + 2; };
     for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
-        if (!tried && m0 >= mine / 2) {
-            tried = true;
-            uint32_t first = 1;
-            if (flane() == 0) first = atomicAdd(&L.mid[j % CIDR], 1u);
-            grab = uni(first) == 0;
-            if (grab && flane() == 0) nx = 2 * C.G + g_add(&C.cc()->next, 1u);
-        }
+        if (!tried && m0 >= mine / 2 && prev_taken()) try_take();
 #pragma unroll
         for (uint32_t u = 0; u < SCAN_D; ++u) {
             const float4 x = v[u];
@@ -439,11 +451,12 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
             }
         }
     }
-    if (!tried && mine == 0 && s == 0) {  // an empty chunk: wave 0 takes it
-        uint32_t first = 1;
-        if (flane() == 0) first = atomicAdd(&L.mid[j % CIDR], 1u);
-        grab = uni(first) == 0;
-        if (grab && flane() == 0) nx = 2 * C.G + g_add(&C.cc()->next, 1u);
+    if (!tried) {  // no steps here (a short chunk) or slot j - 1's take came late
+        for (uint32_t spins = 0; !prev_taken(); ++spins) {
+            __builtin_amdgcn_s_sleep(1);
+            if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(8)); break; }
+        }
+        try_take();
     }
     if (grab && flane() == 0) {
         // slot j + NBUF reuses slot j - NBUF's counter: every wave is done
@@ -511,7 +524,7 @@ __device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, ui
                     a = ld_sc1(&C.A.desc[d.cs + p0 + i].agg);
                     pend = (uint32_t)(a >> 32) != tA;
                 }
-                if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+                if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(2)); break; }
             }
             if (i < n) { pq += (uint32_t)(a >> 16) & 0xffffu; pw += (uint32_t)a & 0xffffu; }
         }
@@ -550,7 +563,7 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
     }
     for (uint32_t spins = 0; lds_ld(&L.sdone[par]) < NS; ++spins) {
         __builtin_amdgcn_s_sleep(1);
-        if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+        if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(3)); break; }
     }
     if (STAGE == 1 || STAGE == 3) {
         release(C, par, j);
@@ -1125,7 +1138,7 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
     for (uint32_t spins = 0; (uint32_t)(w0 >> 32) != tD; ++spins) {
         __builtin_amdgcn_s_sleep(2);
         w0 = ld_sc1(&D.w[0]);
-        if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); return; }
+        if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(4)); return; }
     }
     const uint32_t flags = uni((uint32_t)w0);
     if (!(flags & DEC_B)) return;
@@ -1149,7 +1162,7 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
         BucketCtl *bc = &C.cc()->bk[b];
         for (uint32_t spins = 0; ld_acq_relaxed(&bc->lists) < d.nc; ++spins) {
             __builtin_amdgcn_s_sleep(2);
-            if (spins > SPIN_MAX) { if (lane == 0) C.fail(FAIL_SPIN_TIMEOUT); return; }
+            if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(5)); return; }
         }
         if (b < 16) C.stamp(64 + 4 * b + 1, 0);
         rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
@@ -1200,7 +1213,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
             uint32_t spins = 0;
             for (; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(6)); break; }
             }
             if (C.stamping && spins && flane() == 0) atomicAdd(&L.stamp[121], spins);
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
@@ -1214,7 +1227,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
         for (uint32_t j = 0;; ++j) {
             for (uint32_t spins = 0; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(FAIL_SPIN_TIMEOUT); break; }
+                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(7)); break; }
             }
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
             if (k >= A.K) break;

@@ -222,17 +222,24 @@ BATCH = [
 ]
 
 
-@pytest.mark.parametrize("layout", ["mixed", "sixteen"])
+@pytest.mark.parametrize("layout", ["mixed", "sixteen", "short_chunks"])
 def test_thresholdv16_batch(gpu, oracle, layout):
     import torch
     from stellatrain_amd import ThresholdvCompressor16
+    iters = 7
     if layout == "mixed":
         spec = BATCH
-    else:  # a full batch of 16 distinct keys, then one more (17 -> two launches)
+    elif layout == "sixteen":  # a full batch of 16 distinct keys, then one more (17 -> two launches)
         spec = [(f"s{i}@w", 131072 + 16 * i + (i % 3), 1311 + i, D1 if i % 2 else D2, 0) for i in range(17)]
+    else:
+        # more chunks than two per workgroup (dynamic chunk takes) and every
+        # bucket ending in a short chunk: streaming waves with no lines there
+        # must not take chunks out of order (the C4 layout's failure mode)
+        spec = [(f"c{i}@w", (65 << 15) + 16 * 37 * i + 5 + 16 * (i % 4), 21300 + i, D1, 0) for i in range(16)]
+        iters = 4
     comp = ThresholdvCompressor16()
     ho = oracle.tv16_new()
-    for it in range(7):
+    for it in range(iters):
         items, ref = [], []
         for j, (key, n, k, dist, off) in enumerate(spec):
             src = synth(n, seed_for(40 + j, it), dist)
