@@ -92,7 +92,10 @@ struct Workspace {
         const size_t o_cand = carve(sizeof(uint64_t) * stg::SORT_CAP);
         const size_t o_misc = carve(sizeof(uint32_t) * 64);
         HIP_TRY(hipMalloc(&fixed, off));
-        HIP_TRY(hipMemset(fixed, 0, off));
+        // zeroed on this workspace's stream: the launches that read the
+        // control block are ordered after it (a plain hipMemset runs on the
+        // null stream, which a non-blocking stream does not wait for)
+        HIP_TRY(hipMemsetAsync(fixed, 0, off, stream));
         char *b = static_cast<char *>(fixed);
         d.ctl = reinterpret_cast<stg::FillCtl *>(b + o_ctl);
         d.cp = reinterpret_cast<stg::CallParams *>(b + o_cp);
@@ -122,7 +125,7 @@ struct Workspace {
         if (n <= cap_desc) return STG_OK;
         int rc;
         if ((rc = grow(d.desc, cap_desc, n))) return rc;
-        HIP_TRY(hipMemset(d.desc, 0, cap_desc * sizeof(stg::ChunkDesc)));
+        HIP_TRY(hipMemsetAsync(d.desc, 0, cap_desc * sizeof(stg::ChunkDesc), stream));
         return STG_OK;
     }
 
@@ -191,7 +194,9 @@ struct stg_codec {
         if (nslots % SLOTS_PER_CHUNK == 0) {
             KeyState *c = nullptr;
             HIP_TRY(hipMalloc(&c, sizeof(KeyState) * SLOTS_PER_CHUNK));
-            HIP_TRY(hipMemset(c, 0, sizeof(KeyState) * SLOTS_PER_CHUNK));
+            // states are read on any stream: zero them before any launch sees them
+            HIP_TRY(hipMemsetAsync(c, 0, sizeof(KeyState) * SLOTS_PER_CHUNK, nullptr));
+            HIP_TRY(hipStreamSynchronize(nullptr));
             chunks.push_back(c);
         }
         const uint32_t s = nslots++;
@@ -564,12 +569,25 @@ int stg_codec_check(stg_codec_t h) {
     std::lock_guard<std::mutex> g(h->mu);
     for (auto &kv : h->ws) {
         HIP_TRY(hipStreamSynchronize(kv.first));
-        uint32_t f = 0;
-        HIP_TRY(hipMemcpy(&f, kv.second->d.fail, sizeof f, hipMemcpyDeviceToHost));
-        if (f) {
-            char b[96];
-            snprintf(b, sizeof b, "device failure flags 0x%x", f);
-            return fail(STG_ERR_DEVICE, b);
+        uint32_t f[48] = {};
+        HIP_TRY(hipMemcpy(f, kv.second->d.fail, sizeof f, hipMemcpyDeviceToHost));
+        if (f[0]) {
+            std::string m = "device failure flags 0x";
+            char b[160];
+            snprintf(b, sizeof b, "%x", f[0]);
+            m += b;
+            if (f[1]) {  // spin-timeout records (tv16.hip Ctx::spin_fail)
+                snprintf(b, sizeof b, " (first spin timeout: site %u, workgroup %u, %u %u %u, epoch %u)", f[1] - 1, f[2],
+                         f[3], f[4], f[5], f[6]);
+                m += b;
+                for (uint32_t site = 0; site < 10; ++site) {
+                    const uint32_t *r = f + 8 + 4 * site;
+                    if (!r[0]) continue;
+                    snprintf(b, sizeof b, " [site %u: wg %u, %u %u %u]", site, r[0] - 1, r[1], r[2], r[3]);
+                    m += b;
+                }
+            }
+            return fail(STG_ERR_DEVICE, m);
         }
     }
     return STG_OK;

@@ -67,6 +67,12 @@ constexpr uint32_t NBUF = STG_TV16_NBUF;  // LDS buffer sets (slots) in flight p
 constexpr uint32_t CIDR = 2 * NBUF;       // chunk-id ring
 constexpr uint32_t STAGE_B = 88;    // qualifying lines staged in LDS per slot (~20 expected at 1%)
 constexpr uint32_t WL_B = 64;       // window candidates listed in LDS per slot
+#ifndef STG_TV16_POLL_SLEEP
+#define STG_TV16_POLL_SLEEP 8  // s_sleep units (64 clocks) between prefix polls
+#endif
+#ifndef STG_TV16_DEC_SLEEP
+#define STG_TV16_DEC_SLEEP 16  // between a ranker's polls of the next decision
+#endif
 #ifndef STG_TV16_PRIO
 #define STG_TV16_PRIO 1
 #endif
@@ -83,7 +89,16 @@ constexpr uint32_t SCAN_D = STG_TV16_SCAN_D;
 constexpr uint32_t MAXG = 512;      // workgroups per launch (2 per CU)
 constexpr uint32_t L1_SHIFT = 14;   // level-1 bin width in ulps below t (~0.2% of t)
 constexpr uint32_t WIN = 1u << 17;  // regime-B window below t, in ulps (~1.6% of t)
-constexpr uint32_t SPIN_MAX = 1u << 22;
+// Bounded waits give up after SPIN_TICKS of the 100 MHz s_memrealtime clock
+// (read every 64 polls, from the first poll on): the same wall-clock limit at
+// every site, so the wait that started first also gives up first.
+constexpr uint64_t SPIN_TICKS = 20000000;  // 200 ms
+__device__ __forceinline__ bool spin_expired(uint32_t spins, uint64_t &t0) {
+    if (spins & 63u) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (spins == 0) { t0 = now; return false; }
+    return now - t0 > SPIN_TICKS;
+}
 static_assert(SORT_CAP == MAX_BATCH * CAND_CAP, "one candidate slot per bucket of a launch");
 
 // ---------------------------------------------------------------------------
@@ -292,6 +307,25 @@ struct Ctx {
     __device__ __forceinline__ CallCtl *cc() const { return &ctlp->cc[A.epoch & 1u]; }
     __device__ __forceinline__ uint64_t *cand(uint32_t b) const { return candp + (size_t)b * CAND_CAP; }
     __device__ __forceinline__ void fail(uint32_t bits) const { g_or(failp, bits); }
+    // A spin timeout: its site bit, and for the first one in the workspace's
+    // life a record for the host's error message: {site + 1, workgroup, x0,
+    // x1, x2, epoch} at fail[1..6]; per site, its first one at fail[8 + 4 site].
+    __device__ __forceinline__ void spin_fail(uint32_t site, uint32_t x0, uint32_t x1, uint32_t x2) const {
+        g_or(failp, spin_site(site));
+        if (atomicCAS(failp + 1, 0u, site + 1u) == 0u) {
+            st_sc1(failp + 2, w);
+            st_sc1(failp + 3, x0);
+            st_sc1(failp + 4, x1);
+            st_sc1(failp + 5, x2);
+            st_sc1(failp + 6, A.epoch);
+        }
+        uint32_t *rec = failp + 8 + 4 * site;  // and each site's first one: {workgroup + 1, x0, x1, x2}
+        if (atomicCAS(rec, 0u, w + 1u) == 0u) {
+            st_sc1(rec + 1, x0);
+            st_sc1(rec + 2, x1);
+            st_sc1(rec + 3, x2);
+        }
+    }
     __device__ __forceinline__ void stamp(uint32_t slot, uint32_t v) const {
         if (stamping && slot < 128 && flane() == 0) L.stamp[slot] = v ? v : (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
@@ -318,9 +352,10 @@ struct Ctx {
             for (uint32_t i = lane; i < G; i += 64) st_sc1(&fc->slot[i].go, go);
             vm_drain();
         }
+        uint64_t st1 = 0;
         for (uint32_t spins = 0; ld_sc1(&fc->slot[w].go) != go; ++spins) {
             __builtin_amdgcn_s_sleep(1);
-            if (spins > SPIN_MAX) { if (lane == 0) fail(spin_site(0)); break; }
+            if (spin_expired(spins, st1)) { if (lane == 0) spin_fail(0, r, ld_acq_relaxed(&cc()->bar), G); break; }
         }
     }
 };
@@ -339,10 +374,11 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     Lds &L = C.L;
     const uint32_t par = j % NBUF;
     if (j >= NBUF) {  // buffer set `par` is free once the finisher released slot j - NBUF
+        uint64_t st2 = 0;
         uint32_t spins = 0;
         for (; lds_ld(&L.fdone) < j + 1 - NBUF; ++spins) {
             __builtin_amdgcn_s_sleep(2);
-            if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(1)); break; }
+            if (spin_expired(spins, st2)) { if (flane() == 0) C.spin_fail(1, j, lds_ld(&L.fdone), s); break; }
         }
         if (C.stamping && spins && flane() == 0) atomicAdd(&L.stamp[120], spins);
     }
@@ -452,9 +488,10 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
         }
     }
     if (!tried) {  // no steps here (a short chunk) or slot j - 1's take came late
+        uint64_t st3 = 0;
         for (uint32_t spins = 0; !prev_taken(); ++spins) {
             __builtin_amdgcn_s_sleep(1);
-            if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(8)); break; }
+            if (spin_expired(spins, st3)) { if (flane() == 0) C.spin_fail(8, j, lds_ld(&L.cok[(j + 1) % CIDR]), s); break; }
         }
         try_take();
     }
@@ -518,13 +555,30 @@ __device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, ui
             uint64_t a = 0;
             if (i < n) { const uint4 e = L.gb[i]; a = ((uint64_t)e.y << 32) | e.x; }
             bool pend = i < n && (uint32_t)(a >> 32) != tA;
-            for (uint32_t spins = 0; __any(pend); ++spins) {
-                __builtin_amdgcn_s_sleep(4);  // a poll is a memory round trip: do not flood the queues
-                if (pend) {
+            // Stale ones: poll only the latest pending chunk (taken last, so
+            // almost always published last) from one lane, then re-read the
+            // rest once -- every finisher polling every stale descriptor
+            // floods the fabric the streaming loads share.
+            uint64_t st4 = 0;
+            for (uint32_t spins = 0;; ++spins) {
+                const uint64_t pm = __ballot(pend);
+                if (!pm) break;
+                const uint32_t hl = 63u - (uint32_t)__clzll((long long)pm);
+                __builtin_amdgcn_s_sleep(STG_TV16_POLL_SLEEP);
+                if (lane == hl) {
                     a = ld_sc1(&C.A.desc[d.cs + p0 + i].agg);
                     pend = (uint32_t)(a >> 32) != tA;
                 }
-                if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(2)); break; }
+                if (!__ballot(lane == hl && pend) && pend) {
+                    a = ld_sc1(&C.A.desc[d.cs + p0 + i].agg);
+                    pend = (uint32_t)(a >> 32) != tA;
+                }
+                if (spin_expired(spins, st4)) { {
+                    const uint32_t pi = uni((uint32_t)__builtin_amdgcn_readlane((int)(p0 + i), (int)hl));
+                    const uint32_t tg = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), (int)hl);
+                    if (lane == 0) C.spin_fail(2, c, pi, tg);
+                    break;
+                } }
             }
             if (i < n) { pq += (uint32_t)(a >> 16) & 0xffffu; pw += (uint32_t)a & 0xffffu; }
         }
@@ -561,9 +615,10 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
         vm_drain();
         flush_lists(C, F);
     }
+    uint64_t st5 = 0;
     for (uint32_t spins = 0; lds_ld(&L.sdone[par]) < NS; ++spins) {
         __builtin_amdgcn_s_sleep(1);
-        if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(3)); break; }
+        if (spin_expired(spins, st5)) { if (lane == 0) C.spin_fail(3, j, lds_ld(&L.sdone[par]), k); break; }
     }
     if (STAGE == 1 || STAGE == 3) {
         release(C, par, j);
@@ -1135,10 +1190,11 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
     Decision &D = C.ctl()->dec[b];
     const uint32_t tD = C.tag(TAG_DEC);
     uint64_t w0 = ld_sc1(&D.w[0]);
+    uint64_t st6 = 0;
     for (uint32_t spins = 0; (uint32_t)(w0 >> 32) != tD; ++spins) {
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(STG_TV16_DEC_SLEEP);
         w0 = ld_sc1(&D.w[0]);
-        if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(4)); return; }
+        if (spin_expired(spins, st6)) { if (lane == 0) C.spin_fail(4, b, (uint32_t)(w0 >> 32), tD); return; }
     }
     const uint32_t flags = uni((uint32_t)w0);
     if (!(flags & DEC_B)) return;
@@ -1160,9 +1216,10 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
         const uint32_t R = (C.G - g + NG - 1) / NG, r = C.w / NG;
         if (r >= Wtot + (tail ? 1u : 0u)) return;
         BucketCtl *bc = &C.cc()->bk[b];
+        uint64_t st7 = 0;
         for (uint32_t spins = 0; ld_acq_relaxed(&bc->lists) < d.nc; ++spins) {
             __builtin_amdgcn_s_sleep(2);
-            if (spins > SPIN_MAX) { if (lane == 0) C.fail(spin_site(5)); return; }
+            if (spin_expired(spins, st7)) { if (lane == 0) C.spin_fail(5, b, ld_acq_relaxed(&bc->lists), d.nc); return; }
         }
         if (b < 16) C.stamp(64 + 4 * b + 1, 0);
         rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
@@ -1210,10 +1267,11 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave < NS) {
         for (uint32_t j = 0;; ++j) {
+            uint64_t st8 = 0;
             uint32_t spins = 0;
             for (; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(6)); break; }
+                if (spin_expired(spins, st8)) { if (flane() == 0) C.spin_fail(6, j, lds_ld(&L.cok[j % CIDR]), wave); break; }
             }
             if (C.stamping && spins && flane() == 0) atomicAdd(&L.stamp[121], spins);
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
@@ -1225,9 +1283,10 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
         if (STG_TV16_PRIO) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
         FinState F{0};
         for (uint32_t j = 0;; ++j) {
+            uint64_t st9 = 0;
             for (uint32_t spins = 0; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spins > SPIN_MAX) { if (flane() == 0) C.fail(spin_site(7)); break; }
+                if (spin_expired(spins, st9)) { if (flane() == 0) C.spin_fail(7, j, lds_ld(&L.cok[j % CIDR]), 99); break; }
             }
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
             if (k >= A.K) break;
