@@ -99,9 +99,9 @@ def load_traffic(buckets_per_launch: int):
 def main():
     args = parse()
     if args.streams > 1:
-        # two concurrent persistent launches (one 1024-thread workgroup per CU
-        # each): one launch's exchange tail overlaps the other's streaming
-        os.environ.setdefault("STG_TV16_WGPERCU", "1")
+        # S concurrent persistent launches sharing the device's two workgroup
+        # slots per CU: one launch's exchange tail overlaps the others' streaming
+        os.environ.setdefault("STG_TV16_INFLIGHT", str(min(args.streams, 4)))
     import torch
     import torch.distributed as dist
 

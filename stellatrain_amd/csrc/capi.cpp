@@ -258,11 +258,17 @@ struct FusedLane {
 };
 FusedLane g_lanes[64];
 
-uint32_t fused_wg_per_cu() {
+// Fused launches co-resident per device (STG_TV16_INFLIGHT, 1-4; the older
+// STG_TV16_WGPERCU=1 means 2).  The device's two 1024-thread workgroup slots
+// per CU are split evenly between them.
+uint32_t fused_inflight() {
     static const uint32_t v = [] {
+        if (const char *e = getenv("STG_TV16_INFLIGHT")) {
+            const int x = atoi(e);
+            return (uint32_t)std::min(4, std::max(1, x));
+        }
         const char *e = getenv("STG_TV16_WGPERCU");
-        const int x = e ? atoi(e) : 2;
-        return (uint32_t)(x == 1 ? 1 : 2);
+        return (uint32_t)(e && atoi(e) == 1 ? 2 : 1);
     }();
     return v;
 }
@@ -320,11 +326,17 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     a.num_cu = h->num_cu;
     a.ev = timed ? evs.data() : nullptr;
     a.epoch = ws->epoch;
-    a.wg_per_cu = fused_wg_per_cu();
+    // Workgroups are dealt round-robin over the 8 XCDs (32 CUs, 64 slots
+    // each): a launch's share is a multiple of 8 so every XCD holds the same
+    // number of each launch's workgroups and the in-flight launches fit
+    // (170 + 170 + 170 would put 66 on XCD 0 and leave two unresident).
+    const uint32_t inflight = fused_inflight();
+    constexpr uint32_t XCDS = 8;
+    a.max_wg = std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / inflight * XCDS);
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     FusedLane &lane = g_lanes[h->device & 63];
     std::lock_guard<std::mutex> lg(lane.mu);
-    const size_t max_inflight = a.wg_per_cu == 1 ? 2 : 1;
+    const size_t max_inflight = inflight;
     while (lane.inflight.size() >= max_inflight) {
         auto old = lane.inflight.front();
         lane.inflight.erase(lane.inflight.begin());

@@ -168,6 +168,12 @@ __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
 __device__ __forceinline__ uint32_t g_add(uint32_t *p, uint32_t v) {
     return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint64_t g_add(uint64_t *p, uint64_t v) {
+    return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_acq_relaxed(const uint64_t *p) {
+    return __hip_atomic_load(gp(const_cast<uint64_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ uint32_t g_or(uint32_t *p, uint32_t v) {
     return __hip_atomic_fetch_or(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -65,10 +65,30 @@ static_assert(RNK == FNW - 1, "one streaming group, one finisher, one ranker");
 #endif
 constexpr uint32_t NBUF = STG_TV16_NBUF;  // LDS buffer sets (slots) in flight per workgroup
 constexpr uint32_t CIDR = 2 * NBUF;       // chunk-id ring
-constexpr uint32_t STAGE_B = 88;    // qualifying lines staged in LDS per slot (~20 expected at 1%)
-constexpr uint32_t WL_B = 64;       // window candidates listed in LDS per slot
+#ifndef STG_TV16_STAGE_B
+#define STG_TV16_STAGE_B 88
+#endif
+#ifndef STG_TV16_WL_B
+#define STG_TV16_WL_B 64
+#endif
+constexpr uint32_t STAGE_B = STG_TV16_STAGE_B;  // qualifying lines staged in LDS per slot (~20 expected at 1%)
+constexpr uint32_t WL_B = STG_TV16_WL_B;  // window candidates listed in LDS per slot
 #ifndef STG_TV16_POLL_SLEEP
 #define STG_TV16_POLL_SLEEP 8  // s_sleep units (64 clocks) between prefix polls
+#endif
+// diagnostics only (timing attribution; wrong results): skip the prefix waits
+// or the ordered emission
+#ifndef STG_TV16_DIAG_NOWAIT
+#define STG_TV16_DIAG_NOWAIT 0
+#endif
+#ifndef STG_TV16_DIAG_NOEMIT
+#define STG_TV16_DIAG_NOEMIT 0
+#endif
+#ifndef STG_TV16_LAST_FLUSH
+#define STG_TV16_LAST_FLUSH 1
+#endif
+#ifndef STG_TV16_PREPARE
+#define STG_TV16_PREPARE 1
 #endif
 #ifndef STG_TV16_DEC_SLEEP
 #define STG_TV16_DEC_SLEEP 16  // between a ranker's polls of the next decision
@@ -179,6 +199,7 @@ struct Lds {
     uint32_t fdone;                      // slots released by the finisher
     // finisher
     uint4 gb[GB];                        // gathered chunk descriptors (one piece of a bucket)
+    uint32_t pw[MAX_BATCH];              // window lines of the pending (uncounted) lists, by bucket
     // ranker
     union {
         uint64_t cand[CAND_CAP];         // rare path: candidate set (u64 composite keys)
@@ -360,7 +381,7 @@ struct Ctx {
     }
 };
 
-constexpr uint32_t TAG_AGG = 1, TAG_DEC = 3, TAG_TIE = 4;
+constexpr uint32_t TAG_AGG = 1, TAG_DEC = 3, TAG_TIE = 4, TAG_RDY = 5;
 constexpr uint32_t DEC_B = 1, DEC_WIN = 2, DEC_TAIL = 4;
 
 // ===========================================================================
@@ -562,7 +583,7 @@ __device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, ui
             uint64_t st4 = 0;
             for (uint32_t spins = 0;; ++spins) {
                 const uint64_t pm = __ballot(pend);
-                if (!pm) break;
+                if (!pm || STG_TV16_DIAG_NOWAIT) break;
                 const uint32_t hl = 63u - (uint32_t)__clzll((long long)pm);
                 __builtin_amdgcn_s_sleep(STG_TV16_POLL_SLEEP);
                 if (lane == hl) {
@@ -588,7 +609,8 @@ __device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, ui
 }
 
 // Per-finisher state carried between slots: window lists written but not yet
-// counted (their stores are retired by the next gather), 4 bits per bucket.
+// counted (their stores are retired by the next gather), 4 bits per bucket;
+// their window lines are summed in L.pw.
 struct FinState {
     uint64_t pend;
 };
@@ -597,7 +619,10 @@ struct FinState {
 __device__ __forceinline__ void flush_lists(Ctx &C, FinState &F) {
     for (uint32_t b = 0; F.pend; ++b, F.pend >>= 4) {
         const uint32_t n = (uint32_t)(F.pend & 15u);
-        if (n && flane() == 0) g_add(&C.cc()->bk[b].lists, n);
+        if (n && flane() == 0) {
+            g_add(&C.cc()->bk[b].listed, ((uint64_t)n << 32) | C.L.pw[b]);
+            C.L.pw[b] = 0;
+        }
     }
 }
 
@@ -646,7 +671,7 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
     const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
     const uint32_t lim = kb + (r ? 1u : 0u);
     const bool vec = aligned16(d);
-    if (P < lim && qw) {
+    if (P < lim && qw && !STG_TV16_DIAG_NOEMIT) {
         if (qw <= STAGE_B) {
             // every qualifying line is staged in LDS with its line index: its
             // in-chunk rank is the number of staged lines before it; a quad
@@ -738,6 +763,11 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
         flush_lists(C, F);
     }
     F.pend += 1ull << (4 * b);
+    if (lane == 0) L.pw[b] += ww;
+    if (STG_TV16_LAST_FLUSH && c + 1 == d.nc) {  // the bucket's last list: count it now, the rankers wait for it
+        vm_drain();
+        flush_lists(C, F);
+    }
     release(C, par, j);
     if (j < 16) C.stamp(j * 4 + 2, 0);
 
@@ -1182,11 +1212,173 @@ __device__ __forceinline__ void rank_rare(Ctx &C, uint32_t b, uint32_t flags, ui
     }
 }
 
+// Window path, ahead of the decision.  Once every chunk of the bucket has
+// counted its window list, the W listed lines are known; the ranker gathers
+// the set, counting-sorts it, ranks its entries r, r + R, ... within the set
+// and stages their lines in LDS -- before the bucket's regime is decided, so
+// that after the decision only the output offsets remain (the batch's last
+// bucket is otherwise a serial tail of three memory round trips).  Work for a
+// bucket that ends in regime A, or on the rare path, is dropped.
+struct WinPrep {
+    uint32_t ne;  // entries prepared (0: not prepared)
+    bool lines;   // their lines are staged in LDS (aligned bucket)
+};
+
+__device__ __forceinline__ void win_prepare(Ctx &C, uint32_t r, uint32_t R, const BucketDesc &d, uint32_t b,
+                                            uint32_t W, WinPrep &P) {
+    Lds &L = C.L;
+    const uint32_t lane = flane();
+    const uint32_t *ckey = reinterpret_cast<const uint32_t *>(C.cand(b));
+    const uint32_t *cpos = ckey + CAND_CAP;
+    const uint32_t ne = (W - r + R - 1) / R;
+    if (ne > 64) return;  // more than one entry per lane: the post-decision path
+    gather16(ckey, (W + 3) / 4, L.wr.key);
+    for (uint32_t i = lane; i < WBINS; i += 64) L.wr.bin[i] = 0;
+    lds_drain();
+    constexpr uint32_t SH = 29 - 10;  // keys < 2^29
+    for (uint32_t i = lane; i < W; i += 64) atomicAdd(&L.wr.bin[L.wr.key[i] >> SH], 1u);
+    lds_drain();
+    {  // exclusive scan of the bins, 16 per lane
+        constexpr uint32_t BPL = WBINS / 64;
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < BPL; ++q) sum += L.wr.bin[lane * BPL + q];
+        uint32_t run = wave_incl_scan(sum) - sum;
+        for (uint32_t q = 0; q < BPL; ++q) {
+            const uint32_t c = L.wr.bin[lane * BPL + q];
+            L.wr.bin[lane * BPL + q] = run;
+            run += c;
+        }
+    }
+    lds_drain();
+    for (uint32_t i = lane; i < W; i += 64) {
+        const uint32_t k = L.wr.key[i];
+        L.wr.srt[atomicAdd(&L.wr.bin[k >> SH], 1u)] = k;  // bin[x] ends as the end of bin x
+    }
+    lds_drain();
+    if (lane < ne) {
+        const uint32_t k = L.wr.key[r + lane * R];
+        const uint32_t bn = k >> SH;
+        const uint32_t lo = bn ? L.wr.bin[bn - 1] : 0u, hi = L.wr.bin[bn];
+        uint32_t rank = lo;
+        for (uint32_t x = lo; x < hi; ++x) rank += L.wr.srt[x] < k;
+        L.wr.ent[lane] = make_uint4(rank, ld_sc1(&cpos[k & 0xfffu]), 0u, k);
+    }
+    lds_drain();
+    P.ne = ne;
+    P.lines = aligned16(d);
+    if (P.lines) {  // stage the lines (a quad of lanes per entry) where the keys were
+        float4 *lines = reinterpret_cast<float4 *>(L.wr.key);
+        const uint32_t c4 = 4 * (lane & 3);
+        float4 x[4];
+#pragma unroll
+        for (uint32_t g0 = 0; g0 < 4; ++g0) {
+            const uint32_t el = g0 * 16 + (lane >> 2);
+            x[g0] = el < ne ? *reinterpret_cast<const float4 *>(d.src + (size_t)L.wr.ent[el].y + c4)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (uint32_t g0 = 0; g0 < 4; ++g0) lines[(g0 * 16 + (lane >> 2)) * 4 + (lane & 3)] = x[g0];
+        lds_drain();
+    }
+}
+
+// Window path after the decision, for a prepared ranker: offsets from the
+// bucket's count, the ragged tail (set index W) inserted into the order when it
+// competes, and the stores.
+__device__ __forceinline__ void win_emit(Ctx &C, uint32_t r, uint32_t R, const BucketDesc &d, uint32_t cnt, uint32_t W,
+                                         bool tail, float tail_key, uint32_t tb, const WinPrep &P) {
+    Lds &L = C.L;
+    const uint32_t lane = flane();
+    constexpr uint32_t SH = 29 - 10;
+    const uint32_t wlo = tb > WIN ? tb - WIN : 0u;
+    const uint32_t ut = f2u(tail_key);  // a negative tail key has the sign bit: never in the window
+    const bool tail_in = tail && ut >= wlo && ut < tb && W < CAND_CAP;
+    const uint32_t tail_k = ((tb - 1u - ut) << 12) | W;
+    const uint32_t tailpos = d.nb * 16;
+    const uint32_t c4 = 4 * (lane & 3);
+    const float4 *lines = reinterpret_cast<const float4 *>(L.wr.key);
+#pragma unroll
+    for (uint32_t g0 = 0; g0 < 4; ++g0) {
+        const uint32_t el = g0 * 16 + (lane >> 2);
+        if (el >= P.ne) break;
+        const uint4 en = L.wr.ent[el];
+        const bool tb4 = tail_in && tail_k < en.w;  // the tail sorts before this entry
+        const uint64_t off = (uint64_t)cnt + 16ull * (en.x + (tb4 ? 1u : 0u)) - (tb4 ? (uint64_t)(16u - d.tl) : 0ull);
+        if (off >= d.dst_len) continue;
+        const uint32_t len = std::min<uint32_t>(16u, d.dst_len - (uint32_t)off);
+        const uint32_t bi = en.y + c4 + (uint32_t)d.idx_offset;
+        if (P.lines && len == 16) {
+            *reinterpret_cast<float4 *>(d.val + off + c4) = lines[el * 4 + (lane & 3)];
+            *reinterpret_cast<uint4 *>(d.idx + off + c4) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+        } else {
+            for (uint32_t cc = 0; cc < 4; ++cc) {
+                if (c4 + cc < len) {
+                    d.val[off + c4 + cc] = d.src[(size_t)en.y + c4 + cc];
+                    d.idx[off + c4 + cc] = bi + cc;
+                }
+            }
+        }
+    }
+    if (tail_in && W % R == r) {  // the tail is this ranker's entry: its rank among the set
+        const uint32_t bn = tail_k >> SH;
+        const uint32_t lo = bn ? L.wr.bin[bn - 1] : 0u, hi = L.wr.bin[bn];
+        uint32_t less = 0;
+        for (uint32_t x = lo + lane; x < hi; x += 64) less += L.wr.srt[x] < tail_k;
+        const uint32_t rank = lo + uni(wave_sum(less));
+        const uint64_t off = (uint64_t)cnt + 16ull * rank;
+        if (off < d.dst_len) {
+            const uint32_t len = std::min<uint32_t>(d.tl, d.dst_len - (uint32_t)off);
+            if (lane < len) {
+                d.val[off + lane] = d.src[(size_t)tailpos + lane];
+                d.idx[off + lane] = tailpos + lane + (uint32_t)d.idx_offset;
+            }
+        }
+    }
+}
+
 // The heap fill of bucket b, run by every ranker once the bucket's decision
-// is posted.
+// is posted (the window path's group prepares ahead of it).
+template <int STAGE>
 __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
     const BucketDesc &d = C.A.bk[b];
     const uint32_t lane = flane();
+    // RK rankers per bucket on the window path (a rotating group, so the set
+    // is fetched RK times rather than G times)
+    const uint32_t NG = std::max(1u, C.G / RK);
+    const uint32_t g = b % NG;
+    const bool grp = C.w % NG == g;
+    const uint32_t R = (C.G - g + NG - 1) / NG, r = C.w / NG;
+    WinPrep P{0, false};
+    uint32_t W = 0;
+    if (STG_TV16_PREPARE && grp && STAGE != 5) {
+        // the group's first ranker alone polls the finishers' list counter
+        // (polling a line under atomic adds slows the adds), then posts the
+        // bucket's window-line count for the others
+        ReadyLine &RL = C.ctl()->ready[b];
+        const uint32_t tR = C.tag(TAG_RDY);
+        uint64_t st7 = 0;
+        if (r == 0) {
+            BucketCtl *bc = &C.cc()->bk[b];
+            uint64_t ls = ld_acq_relaxed(&bc->listed);
+            for (uint32_t spins = 0; (uint32_t)(ls >> 32) < d.nc; ++spins) {
+                __builtin_amdgcn_s_sleep(STG_TV16_DEC_SLEEP);
+                ls = ld_acq_relaxed(&bc->listed);
+                if (spin_expired(spins, st7)) { if (lane == 0) C.spin_fail(5, b, (uint32_t)(ls >> 32), d.nc); return; }
+            }
+            W = uni((uint32_t)ls);
+            if (lane == 0) st_sc1(&RL.w, ((uint64_t)tR << 32) | W);
+        } else {
+            uint64_t rw = ld_sc1(&RL.w);
+            for (uint32_t spins = 0; (uint32_t)(rw >> 32) != tR; ++spins) {
+                __builtin_amdgcn_s_sleep(STG_TV16_DEC_SLEEP);
+                rw = ld_sc1(&RL.w);
+                if (spin_expired(spins, st7)) { if (lane == 0) C.spin_fail(5, b, 0, d.nc); return; }
+            }
+            W = uni((uint32_t)rw);
+        }
+        if (b < 16) C.stamp(64 + 4 * b + 1, 0);
+        if (W > 0 && W + 1 <= CAND_CAP && r < W) win_prepare(C, r, R, d, b, W, P);
+    }
     Decision &D = C.ctl()->dec[b];
     const uint32_t tD = C.tag(TAG_DEC);
     uint64_t w0 = ld_sc1(&D.w[0]);
@@ -1205,24 +1397,23 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
     const float t = __uint_as_float(uni((uint32_t)w3));
     if (b < 16) C.stamp(64 + 4 * b, 0);
     if (flags & DEC_WIN) {
-        // the window holds the top M; every chunk wrote its window lines at
-        // its exchanged offset -- wait for all of them, rank this share
-        // RK rankers per bucket (a rotating group, so the set is fetched RK
-        // times rather than G times)
+        // the window holds the top M: every chunk wrote its window lines at
+        // its exchanged offset (all counted before W was read)
         const bool tail = (flags & DEC_TAIL) != 0;
-        const uint32_t NG = std::max(1u, C.G / RK);
-        const uint32_t g = b % NG;
-        if (C.w % NG != g) return;
-        const uint32_t R = (C.G - g + NG - 1) / NG, r = C.w / NG;
-        if (r >= Wtot + (tail ? 1u : 0u)) return;
-        BucketCtl *bc = &C.cc()->bk[b];
-        uint64_t st7 = 0;
-        for (uint32_t spins = 0; ld_acq_relaxed(&bc->lists) < d.nc; ++spins) {
-            __builtin_amdgcn_s_sleep(2);
-            if (spin_expired(spins, st7)) { if (lane == 0) C.spin_fail(5, b, ld_acq_relaxed(&bc->lists), d.nc); return; }
+        if (!grp || r >= Wtot + (tail ? 1u : 0u)) return;
+        if (P.ne && W == Wtot) {
+            win_emit(C, r, R, d, cnt, Wtot, tail, tail_key, f2u(t), P);
+        } else {
+            BucketCtl *bc = &C.cc()->bk[b];
+            uint64_t st8 = 0;
+            // (with the ready line, every list was already counted)
+            for (uint32_t spins = 0; !(STG_TV16_PREPARE && STAGE != 5) &&
+                                     (uint32_t)(ld_acq_relaxed(&bc->listed) >> 32) < d.nc; ++spins) {
+                __builtin_amdgcn_s_sleep(2);
+                if (spin_expired(spins, st8)) { if (lane == 0) C.spin_fail(5, b, 0, d.nc); return; }
+            }
+            rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
         }
-        if (b < 16) C.stamp(64 + 4 * b + 1, 0);
-        rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
     } else {
         rank_rare(C, b, flags, cnt, M, t, tail_key);
     }
@@ -1252,6 +1443,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
         L.wcnt[threadIdx.x] = 0;
         L.sdone[threadIdx.x] = 0;
     }
+    if (threadIdx.x < MAX_BATCH) L.pw[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         L.fdone = 0;
         // slots 0 and 1: chunks w and G + w; later slots take the next chunks
@@ -1300,7 +1492,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
         if (STAGE != 1 && STAGE != 3) {
             for (uint32_t b = 0; b < A.nbk; ++b) {
                 asm volatile("" : "+s"(C.w), "+s"(C.G), "+s"(C.ctlp), "+s"(C.candp), "+s"(C.failp));
-                rank_bucket(C, b);
+                rank_bucket<STAGE>(C, b);
             }
         }
         if (STAGE == 4) {
@@ -1352,11 +1544,10 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     A.cand = ws.cand;
     A.fail = ws.fail;
     A.stamps = a.b[a.nb - 1].count_out + 1;  // STAGE 4: words after the last bucket's count
-    // wg_per_cu 1024-thread workgroups per CU (2: 32 waves, full occupancy for
-    // one stream; 1: two launches from two streams share the CUs), all
-    // co-resident for the in-launch exchanges; no more than there are chunks
-    const uint32_t G = std::max<uint32_t>(
-        1, std::min<uint32_t>(std::min<uint32_t>(a.wg_per_cu * (uint32_t)a.num_cu, K), MAXG));
+    // this launch's share of the device's two 1024-thread workgroups per CU
+    // (all of them for one stream; launches from several streams split them),
+    // all co-resident for the in-launch exchanges; no more than there are chunks
+    const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(a.max_wg, K), MAXG));
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     switch (dbg_stage) {

@@ -33,8 +33,8 @@ constexpr uint32_t MAX_BATCH = 16;
 constexpr uint32_t TV16_CHUNK = 2048;        // lines (16 floats) per chunk = 128 KiB
 struct BucketCtl {
     uint32_t cand_n;    // regime-B candidates appended (rare paths only)
-    uint32_t lists;     // chunks whose window lists are in place
-    uint32_t pad[2];
+    uint32_t pad;
+    uint64_t listed;    // {chunks whose window lists are in place:32 | their window lines:32}
     uint32_t hist[MAX_LEVELS][HBINS];
 };
 struct CallCtl {
@@ -54,9 +54,17 @@ struct alignas(128) WgSlot {
 struct alignas(32) Decision {
     uint64_t w[4];      // [1] = {cnt:32 | M:32}, [2] = {Wtot:32 | tail key bits:32}, [3] = {Qtot:32 | t bits:32}
 };
+// Per-bucket "window lists complete" word {tag:32 | window lines:32}, written
+// by one ranker (the only poller of the list counter the finishers add to) and
+// polled by the rest of its group: one 128-byte line each.
+struct alignas(128) ReadyLine {
+    uint64_t w;
+    uint64_t pad[15];
+};
 struct FillCtl {
     CallCtl cc[2];                     // [epoch parity]
     Decision dec[MAX_BATCH];
+    ReadyLine ready[MAX_BATCH];
     WgSlot slot[MAX_FILL_WG];
 };
 // Per-chunk descriptor (16 B): every word carries the call tag.
@@ -116,7 +124,7 @@ struct Tv16Launch {
     int num_cu;
     hipEvent_t *ev;    // optional [before, mid, after] the codec launch(es)
     uint32_t epoch;    // per-workspace call counter, 1..2^24-1 (hand-off tags)
-    uint32_t wg_per_cu;  // fused-kernel workgroups per CU (1 or 2)
+    uint32_t max_wg;     // fused-kernel workgroups at most (its share of 2 per CU)
     uint32_t desc_cap;   // ChunkDesc entries at ws.desc
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
