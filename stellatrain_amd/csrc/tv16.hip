@@ -84,11 +84,11 @@ constexpr uint32_t WL_B = STG_TV16_WL_B;  // window candidates listed in LDS per
 #ifndef STG_TV16_DIAG_NOEMIT
 #define STG_TV16_DIAG_NOEMIT 0
 #endif
+#ifndef STG_TV16_DIAG_STORES
+#define STG_TV16_DIAG_STORES 0
+#endif
 #ifndef STG_TV16_LAST_FLUSH
 #define STG_TV16_LAST_FLUSH 1
-#endif
-#ifndef STG_TV16_PREPARE
-#define STG_TV16_PREPARE 1
 #endif
 #ifndef STG_TV16_DEC_SLEEP
 #define STG_TV16_DEC_SLEEP 16  // between a ranker's polls of the next decision
@@ -200,6 +200,7 @@ struct Lds {
     // finisher
     uint4 gb[GB];                        // gathered chunk descriptors (one piece of a bucket)
     uint32_t pw[MAX_BATCH];              // window lines of the pending (uncounted) lists, by bucket
+    uint32_t cum[MAX_BATCH];             // counted so far, by bucket: chunks << 16 | window lines
     // ranker
     union {
         uint64_t cand[CAND_CAP];         // rare path: candidate set (u64 composite keys)
@@ -381,7 +382,7 @@ struct Ctx {
     }
 };
 
-constexpr uint32_t TAG_AGG = 1, TAG_DEC = 3, TAG_TIE = 4, TAG_RDY = 5;
+constexpr uint32_t TAG_AGG = 1, TAG_DEC = 3, TAG_TIE = 4, TAG_RDY = 5, TAG_LST = 6;
 constexpr uint32_t DEC_B = 1, DEC_WIN = 2, DEC_TAIL = 4;
 
 // ===========================================================================
@@ -620,8 +621,12 @@ __device__ __forceinline__ void flush_lists(Ctx &C, FinState &F) {
     for (uint32_t b = 0; F.pend; ++b, F.pend >>= 4) {
         const uint32_t n = (uint32_t)(F.pend & 15u);
         if (n && flane() == 0) {
-            g_add(&C.cc()->bk[b].listed, ((uint64_t)n << 32) | C.L.pw[b]);
+            // this workgroup's own line: no other workgroup writes it
+            const uint32_t c0 = C.L.cum[b];
+            const uint32_t ch = (c0 >> 16) + n, wl = std::min(0xffffu, (c0 & 0xffffu) + C.L.pw[b]);
+            C.L.cum[b] = (ch << 16) | wl;
             C.L.pw[b] = 0;
+            st_sc1(&C.ctl()->lst[C.w].w[b], ((uint64_t)C.tag(TAG_LST) << 32) | (ch << 16) | wl);
         }
     }
 }
@@ -758,6 +763,9 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k, Fin
             }
         }
     }
+    if (j < 16) C.stamp(j * 4 + 3, 0);
+#pragma unroll
+    for (uint32_t x = 0; x < STG_TV16_DIAG_STORES; ++x) st_sc1(C.failp + 60 + (x & 3), 0u);  // diagnostics: extra stores
     if (((F.pend >> (4 * b)) & 15u) == 15u) {  // counter full: retire and count now
         vm_drain();
         flush_lists(C, F);
@@ -1350,7 +1358,7 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
     const uint32_t R = (C.G - g + NG - 1) / NG, r = C.w / NG;
     WinPrep P{0, false};
     uint32_t W = 0;
-    if (STG_TV16_PREPARE && grp && STAGE != 5) {
+    if (grp && STAGE != 5) {
         // the group's first ranker alone polls the finishers' list counter
         // (polling a line under atomic adds slows the adds), then posts the
         // bucket's window-line count for the others
@@ -1358,14 +1366,25 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
         const uint32_t tR = C.tag(TAG_RDY);
         uint64_t st7 = 0;
         if (r == 0) {
-            BucketCtl *bc = &C.cc()->bk[b];
-            uint64_t ls = ld_acq_relaxed(&bc->listed);
-            for (uint32_t spins = 0; (uint32_t)(ls >> 32) < d.nc; ++spins) {
+            uint32_t ch = 0, wl = 0;
+            for (uint32_t spins = 0;; ++spins) {
+                ch = 0;
+                wl = 0;
+                for (uint32_t i = lane; i < C.G; i += 64) {
+                    const uint64_t v = ld_sc1(&C.ctl()->lst[i].w[b]);
+                    if ((uint32_t)(v >> 32) == C.tag(TAG_LST)) {
+                        ch += ((uint32_t)v >> 16) & 0xffffu;
+                        const uint32_t x = (uint32_t)v & 0xffffu;
+                        wl += x == 0xffffu ? CAND_CAP : x;  // saturated: too many for the window path
+                    }
+                }
+                ch = uni(wave_sum(ch));
+                wl = uni(wave_sum(wl));
+                if (ch >= d.nc) break;
                 __builtin_amdgcn_s_sleep(STG_TV16_DEC_SLEEP);
-                ls = ld_acq_relaxed(&bc->listed);
-                if (spin_expired(spins, st7)) { if (lane == 0) C.spin_fail(5, b, (uint32_t)(ls >> 32), d.nc); return; }
+                if (spin_expired(spins, st7)) { if (lane == 0) C.spin_fail(5, b, ch, d.nc); return; }
             }
-            W = uni((uint32_t)ls);
+            W = std::min(wl, CAND_CAP);
             if (lane == 0) st_sc1(&RL.w, ((uint64_t)tR << 32) | W);
         } else {
             uint64_t rw = ld_sc1(&RL.w);
@@ -1404,14 +1423,7 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
         if (P.ne && W == Wtot) {
             win_emit(C, r, R, d, cnt, Wtot, tail, tail_key, f2u(t), P);
         } else {
-            BucketCtl *bc = &C.cc()->bk[b];
-            uint64_t st8 = 0;
-            // (with the ready line, every list was already counted)
-            for (uint32_t spins = 0; !(STG_TV16_PREPARE && STAGE != 5) &&
-                                     (uint32_t)(ld_acq_relaxed(&bc->listed) >> 32) < d.nc; ++spins) {
-                __builtin_amdgcn_s_sleep(2);
-                if (spin_expired(spins, st8)) { if (lane == 0) C.spin_fail(5, b, 0, d.nc); return; }
-            }
+            // (the ready line said every list was counted)
             rank_window(C, r, R, d, b, cnt, Wtot, tail, tail_key, f2u(t));
         }
     } else {
@@ -1443,7 +1455,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
         L.wcnt[threadIdx.x] = 0;
         L.sdone[threadIdx.x] = 0;
     }
-    if (threadIdx.x < MAX_BATCH) L.pw[threadIdx.x] = 0;
+    if (threadIdx.x < MAX_BATCH) { L.pw[threadIdx.x] = 0; L.cum[threadIdx.x] = 0; }
     if (threadIdx.x == 0) {
         L.fdone = 0;
         // slots 0 and 1: chunks w and G + w; later slots take the next chunks

@@ -33,8 +33,7 @@ constexpr uint32_t MAX_BATCH = 16;
 constexpr uint32_t TV16_CHUNK = 2048;        // lines (16 floats) per chunk = 128 KiB
 struct BucketCtl {
     uint32_t cand_n;    // regime-B candidates appended (rare paths only)
-    uint32_t pad;
-    uint64_t listed;    // {chunks whose window lists are in place:32 | their window lines:32}
+    uint32_t pad[3];
     uint32_t hist[MAX_LEVELS][HBINS];
 };
 struct CallCtl {
@@ -61,11 +60,18 @@ struct alignas(128) ReadyLine {
     uint64_t w;
     uint64_t pad[15];
 };
+// Per-workgroup window-list counts, one 128-byte line per workgroup (no line
+// is written by two workgroups): [b] = {tag:32 | chunks:16 | window lines:16},
+// cumulative over the call, lines saturating at 0xffff.
+struct alignas(128) WgLists {
+    uint64_t w[MAX_BATCH];
+};
 struct FillCtl {
     CallCtl cc[2];                     // [epoch parity]
     Decision dec[MAX_BATCH];
     ReadyLine ready[MAX_BATCH];
     WgSlot slot[MAX_FILL_WG];
+    WgLists lst[MAX_FILL_WG];
 };
 // Per-chunk descriptor (16 B): every word carries the call tag.
 struct alignas(16) ChunkDesc {

@@ -5,7 +5,8 @@ Run with STG_DEBUG_TV16_STAGE=4: every workgroup records s_memrealtime
 (100 MHz) into 128 words after the last bucket's count:
   [j*4 + 0]  finisher, slot j < 16: the streaming waves are done with the chunk
   [j*4 + 1]  finisher: prefix counts gathered
-  [j*4 + 2]  finisher: chunk emitted, window list written, slot released
+  [j*4 + 3]  finisher: qualifying lines emitted
+  [j*4 + 2]  finisher: window list written, slot released
   [64 + 4b]      ranker, bucket b < 16 (regime B only): decision seen
   [64 + 4b + 1]  ranker: every chunk's window list in place
   [64 + 4b + 2]  ranker: heap fill share emitted
@@ -93,7 +94,8 @@ def main():
     out["slot_released_med"] = [med(j * 4 + 2) for j in range(NJ)]
     out["slot_released_max"] = [mx(j * 4 + 2) for j in range(NJ)]
     out["prefix_us_med"] = [dur(j * 4 + 1, j * 4) for j in range(NJ)]
-    out["emit_us_med"] = [dur(j * 4 + 2, j * 4 + 1) for j in range(NJ)]
+    out["emit_us_med"] = [dur(j * 4 + 3, j * 4 + 1) for j in range(NJ)]
+    out["list_release_us_med"] = [dur(j * 4 + 2, j * 4 + 3) for j in range(NJ)]
     out["rank_decision_med"] = [med(64 + 4 * b) for b in range(NBK)]
     out["rank_lists_in_med"] = [med(64 + 4 * b + 1) for b in range(NBK)]
     out["rank_done_med"] = [med(64 + 4 * b + 2) for b in range(NBK)]
