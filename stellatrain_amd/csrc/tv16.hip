@@ -58,7 +58,7 @@ constexpr uint32_t FIN = NS;        // wave 14: finisher
 constexpr uint32_t RNK = NS + 1;    // wave 15: ranker (regime-B heap fill)
 static_assert(RNK == FNW - 1, "one streaming group, one finisher, one ranker");
 #ifndef STG_TV16_NBUF
-#define STG_TV16_NBUF 4
+#define STG_TV16_NBUF 5
 #endif
 #ifndef STG_TV16_SCAN_D
 #define STG_TV16_SCAN_D 3
@@ -66,7 +66,7 @@ static_assert(RNK == FNW - 1, "one streaming group, one finisher, one ranker");
 constexpr uint32_t NBUF = STG_TV16_NBUF;  // LDS buffer sets (slots) in flight per workgroup
 constexpr uint32_t CIDR = 2 * NBUF;       // chunk-id ring
 #ifndef STG_TV16_STAGE_B
-#define STG_TV16_STAGE_B 88
+#define STG_TV16_STAGE_B 72
 #endif
 #ifndef STG_TV16_WL_B
 #define STG_TV16_WL_B 64
