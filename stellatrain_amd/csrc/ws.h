@@ -92,6 +92,8 @@ struct RSel {
     uint32_t mask;      // which bits are fixed
     uint32_t rank;      // remaining rank (0-based, descending) inside the prefix
     uint32_t cnt_gt;    // keys strictly above the prefix range
+    uint32_t done;      // workgroups done with the current level (the last one picks)
+    uint32_t pad[3];
     uint32_t hist[RS_BINS];
 };
 
