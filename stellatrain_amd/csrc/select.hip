@@ -18,7 +18,13 @@ namespace stg {
 
 namespace {
 
-constexpr uint32_t NCOPY = 4;
+#ifndef STG_RS_LASTBLOCK
+#define STG_RS_LASTBLOCK 0  // 1: the last histogram workgroup picks; 0: one 64-thread pick launch per level
+#endif
+#ifndef STG_RS_NCOPY
+#define STG_RS_NCOPY 4
+#endif
+constexpr uint32_t NCOPY = STG_RS_NCOPY;
 constexpr uint32_t HWG = 1024;  // rs_hist workgroup: one fat workgroup per CU, few global bin atomics
 
 __global__ void __launch_bounds__(STG_WG) rs_init(RSel *st, const uint32_t *d_rank, uint32_t rank) {
@@ -96,12 +102,24 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
     auto add = [&](uint32_t key) {
         if ((key & mask) == prefix) atomicAdd(&hc[(key >> SHIFT) & (NB - 1)], 1u);
     };
-    for (size_t i = (size_t)blockIdx.x * HWG + threadIdx.x; i < m4; i += stride) {
-        const float4 v = a4[i];
-        uint32_t k0 = f2u(v.x) & 0x7fffffffu, k1 = f2u(v.y) & 0x7fffffffu;
-        uint32_t k2 = f2u(v.z) & 0x7fffffffu, k3 = f2u(v.w) & 0x7fffffffu;
-        if (4 * i + 3 == m - 1) k3 &= last_mask;
-        add(k0); add(k1); add(k2); add(k3);
+    // UF float4 loads per thread in flight before any is used
+    constexpr uint32_t UF = 4;
+    for (size_t i0 = (size_t)blockIdx.x * HWG + threadIdx.x; i0 < m4; i0 += UF * stride) {
+        float4 v[UF];
+#pragma unroll
+        for (uint32_t u = 0; u < UF; ++u) {
+            const size_t i = i0 + u * stride;
+            v[u] = i < m4 ? a4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < UF; ++u) {
+            const size_t i = i0 + u * stride;
+            if (i >= m4) break;
+            uint32_t k0 = f2u(v[u].x) & 0x7fffffffu, k1 = f2u(v[u].y) & 0x7fffffffu;
+            uint32_t k2 = f2u(v[u].z) & 0x7fffffffu, k3 = f2u(v[u].w) & 0x7fffffffu;
+            if (4 * i + 3 == m - 1) k3 &= last_mask;
+            add(k0); add(k1); add(k2); add(k3);
+        }
     }
     if (blockIdx.x == 0) {
         for (size_t i = m4 * 4 + threadIdx.x; i < m; i += HWG) {
@@ -122,12 +140,18 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
     // would write back the whole L2): every thread waits for its atomics to
     // complete, then one relaxed atomic counts the workgroup done; the picker
     // reads the bins with agent-scope loads.
+    if (!STG_RS_LASTBLOCK) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0)
         s_last = __hip_atomic_fetch_add(&st->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
     __syncthreads();
     if (s_last && threadIdx.x < 64) pick<SHIFT, NBITS>(st, extra_zeros);
+}
+
+template <int SHIFT, int NBITS>
+__global__ void __launch_bounds__(64) rs_pick(RSel *st, uint64_t extra_zeros) {
+    pick<SHIFT, NBITS>(st, extra_zeros);
 }
 
 }  // namespace
@@ -139,8 +163,11 @@ hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uin
     const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * 2));
     rs_init<<<1, STG_WG, 0, s>>>(ws.rsel, d_rank, rank);
     rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
+    if (!STG_RS_LASTBLOCK) rs_pick<20, 11><<<1, 64, 0, s>>>(ws.rsel, extra_zeros);
     rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
+    if (!STG_RS_LASTBLOCK) rs_pick<9, 11><<<1, 64, 0, s>>>(ws.rsel, extra_zeros);
     rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
+    if (!STG_RS_LASTBLOCK) rs_pick<0, 9><<<1, 64, 0, s>>>(ws.rsel, extra_zeros);
     return hipGetLastError();
 }
 
