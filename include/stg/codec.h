@@ -134,6 +134,14 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
                              float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
                              uint32_t *d_out_count, void *stream);
 
+/* Error feedback of the MERGE compress (engine/modules/compress.cpp:172-186):
+ * after compressing d_grad into numel (idx, val) slots, zero d_grad at every
+ * d_idx[i], i < numel (unwritten slots hold index 0, so element 0 is zeroed
+ * too, as in the reference), and copy the bucket into d_residual.  Both
+ * arrays end identical.  Asynchronous on `stream`. */
+int stg_error_feedback_device(float *d_grad, size_t n, const uint32_t *d_idx, size_t numel, float *d_residual,
+                              void *stream);
+
 /* Sparse SGD (optim/sgd.cpp:34-263 scalar path; options sgd.cpp:265-300).
  * optimize_raw() keeps one momentum buffer per `name` on the device. */
 int stg_sgd_create(int device, float lr, float momentum, float dampening, float weight_decay, int nesterov,

@@ -138,7 +138,69 @@ __global__ void __launch_bounds__(STG_WG) sgd_apply(SgdLaunch a) {
     }
 }
 
+// Error feedback (compress.cpp:172-186): the bucket, with every selected
+// index zeroed, becomes the residual -- and the bucket itself is left zeroed
+// at those indices, as the reference's in-place src[idx[i]] = 0 leaves it.
+// Pass 1 streams grad -> residual (float4, nontemporal); pass 2 zeroes both
+// arrays at the numel indices (slots past the count hold index 0, so
+// element 0 is zeroed too, as in the reference).
+__global__ void __launch_bounds__(STG_WG) ef_copy(const float *__restrict__ grad, float *__restrict__ resid,
+                                                  size_t n) {
+    const size_t n4 = n / 4;
+    const size_t stride = (size_t)gridDim.x * STG_WG;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v *g4 = reinterpret_cast<const f4v *>(grad);
+    f4v *r4 = reinterpret_cast<f4v *>(resid);
+    constexpr uint32_t UF = 4;
+    for (size_t i0 = (size_t)blockIdx.x * STG_WG + threadIdx.x; i0 < n4; i0 += UF * stride) {
+        f4v v[UF];
+#pragma unroll
+        for (uint32_t u = 0; u < UF; ++u) {
+            const size_t i = i0 + u * stride;
+            if (i < n4) v[u] = __builtin_nontemporal_load(g4 + i);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < UF; ++u) {
+            const size_t i = i0 + u * stride;
+            if (i < n4) __builtin_nontemporal_store(v[u], r4 + i);
+        }
+    }
+    if (blockIdx.x == 0)
+        for (size_t i = n4 * 4 + threadIdx.x; i < n; i += STG_WG) resid[i] = grad[i];
+}
+
+__global__ void __launch_bounds__(STG_WG) ef_zero(float *__restrict__ grad, float *__restrict__ resid,
+                                                  const uint32_t *__restrict__ idx, size_t numel, size_t n) {
+    for (size_t j = (size_t)blockIdx.x * STG_WG + threadIdx.x; j < numel; j += (size_t)gridDim.x * STG_WG) {
+        const uint32_t i = idx[j];
+        if (i < n) {
+            grad[i] = 0.f;
+            resid[i] = 0.f;
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
+                                 hipStream_t s) {
+    if (n) {
+        const bool vec = ((reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(resid)) & 15u) == 0;
+        const size_t work = vec ? (n / 4 + STG_WG - 1) / STG_WG : 0;
+        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * 8));
+        if (vec) ef_copy<<<blocks, STG_WG, 0, s>>>(grad, resid, n);
+        else {
+            const hipError_t e = hipMemcpyAsync(resid, grad, n * sizeof(float), hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (numel) {
+        const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((numel + STG_WG - 1) / STG_WG,
+                                                                              (size_t)num_cu * 4));
+        ef_zero<<<blocks, STG_WG, 0, s>>>(grad, resid, idx, numel, n);
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,

@@ -605,6 +605,17 @@ int stg_codec_check(stg_codec_t h) {
     return STG_OK;
 }
 
+int stg_error_feedback_device(float *d_grad, size_t n, const uint32_t *d_idx, size_t numel, float *d_residual,
+                              void *stream) {
+    if ((n && (!d_grad || !d_residual)) || (numel && !d_idx)) return fail(STG_ERR_INVALID, "null argument");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    int ncu = 256;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(stg::launch_error_feedback(d_grad, n, d_idx, numel, d_residual, ncu, static_cast<hipStream_t>(stream)));
+    return STG_OK;
+}
+
 int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t per_rank, int world, size_t n,
                              float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
                              uint32_t *d_out_count, void *stream) {

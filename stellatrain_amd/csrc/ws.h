@@ -195,5 +195,7 @@ struct SgdLaunch {
     bool nesterov;
 };
 hipError_t launch_sgd(const SgdLaunch &a, hipStream_t s);
+hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
+                                 hipStream_t s);
 
 }  // namespace stg

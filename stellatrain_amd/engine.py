@@ -114,9 +114,13 @@ class CodecEngine:
         val = torch.zeros(numel * world, dtype=torch.float32, device=grad.device)
         cnt = self.compressor_.compress_async(key, grad.reshape(-1), numel, idx[:numel], val[:numel], 0)
         if residual is not None:
-            g = grad.view(-1)
-            g.index_fill_(0, idx[:numel].long(), 0.0)
-            residual.view(-1).copy_(g)
+            import ctypes
+            from ._capi import check, lib
+            if residual.numel() != n or residual.dtype != torch.float32 or not residual.is_contiguous():
+                raise ValueError("residual must be a contiguous float32 tensor of the bucket's size")
+            check(lib().stg_error_feedback_device(ctypes.c_void_p(grad.data_ptr()), n, ctypes.c_void_p(idx.data_ptr()),
+                                                  numel, ctypes.c_void_p(residual.data_ptr()),
+                                                  ctypes.c_void_p(torch.cuda.current_stream(grad.device).cuda_stream)))
         return idx, val, cnt
 
 

@@ -171,3 +171,31 @@ def test_error_feedback_residual(gpu, oracle):
         assert np.array_equal(resid.cpu().numpy().view(np.uint32), expect.view(np.uint32))
         assert np.array_equal(g.cpu().numpy().view(np.uint32), expect.view(np.uint32))
     oracle.tv16_free(ho)
+
+
+@pytest.mark.parametrize("n,off,numel", [(1000003, 0, 10000), (4099, 1, 41), (64, 0, 0)])
+def test_error_feedback_kernel(gpu, n, off, numel):
+    """stg_error_feedback_device against a torch fp32 reference of
+    compress.cpp:172-186: zero the bucket at every slot's index (unwritten
+    slots hold index 0), copy it into the residual; ragged and unaligned
+    buckets take the copy fallback."""
+    import ctypes
+    import torch
+    from stellatrain_amd._capi import check, lib
+    gen = torch.Generator().manual_seed(n + off)
+    base = torch.randn(n + off, generator=gen).to(gpu)
+    g = base[off:]
+    idx = torch.zeros(numel, dtype=torch.int32)
+    if numel:
+        idx[: numel - numel // 4] = torch.randperm(n, generator=gen)[: numel - numel // 4].to(torch.int32)
+    idx = idx.to(gpu)
+    expect = g.clone()
+    if numel:
+        expect[idx.long()] = 0.0
+    resid = torch.full((n,), 7.0, dtype=torch.float32, device=gpu)
+    check(lib().stg_error_feedback_device(ctypes.c_void_p(g.data_ptr()), n, ctypes.c_void_p(idx.data_ptr()), numel,
+                                          ctypes.c_void_p(resid.data_ptr()),
+                                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    assert torch.equal(resid, expect)
+    assert torch.equal(g, expect)
