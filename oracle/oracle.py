@@ -134,6 +134,14 @@ class Oracle(_Codecs):
         lib.orc_sgd_apply.argtypes = [C.c_void_p, C.c_char_p, _f32p, C.c_uint32, _f32p, _u32p, C.c_uint32]
         lib.orc_sgd_momentum.restype = C.c_int
         lib.orc_sgd_momentum.argtypes = [C.c_void_p, C.c_char_p, _f32p, C.c_uint32]
+        lib.orc_adam_new.restype = C.c_void_p
+        lib.orc_adam_new.argtypes = [C.c_float] * 5 + [C.c_int, C.c_int]
+        lib.orc_adam_free.restype = None
+        lib.orc_adam_free.argtypes = [C.c_void_p]
+        lib.orc_adam_apply.restype = None
+        lib.orc_adam_apply.argtypes = [C.c_void_p, C.c_char_p, _f32p, C.c_uint32, _f32p, _u32p, C.c_uint32]
+        lib.orc_adam_state.restype = C.c_int
+        lib.orc_adam_state.argtypes = [C.c_void_p, C.c_char_p, _f32p, _f32p, C.c_uint32, C.POINTER(C.c_float)]
         lib.orc_last_error.restype = C.c_char_p
 
     def synth(self, n: int, seed: int, dist: int = 0, param: int = 0) -> np.ndarray:
@@ -192,6 +200,22 @@ class Oracle(_Codecs):
         out = np.zeros(n, np.float32)
         rc = self.lib.orc_sgd_momentum(h, name.encode(), out, n)
         return None if rc else out
+
+    def adam_new(self, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, weight_decay=0.0, amsgrad=False, maximize=False):
+        return self.lib.orc_adam_new(lr, b1, b2, eps, weight_decay, int(amsgrad), int(maximize))
+
+    def adam_free(self, h):
+        self.lib.orc_adam_free(h)
+
+    def adam_apply(self, h, name, param, g, gidx):
+        self.lib.orc_adam_apply(h, name.encode(), param, param.size, np.ascontiguousarray(g, np.float32),
+                                np.ascontiguousarray(gidx, np.uint32), len(g))
+
+    def adam_state(self, h, name, n):
+        """(m, v, vmax, tick) of a name, or None before its first call."""
+        m, v, vmax = np.zeros(n, np.float32), np.zeros(n, np.float32), C.c_float()
+        tick = self.lib.orc_adam_state(h, name.encode(), m, v, n, C.byref(vmax))
+        return None if tick < 0 else (m, v, np.float32(vmax.value), tick)
 
 
 class Reference(_Codecs):

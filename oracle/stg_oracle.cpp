@@ -21,6 +21,7 @@
  *   - top-k       : compress/topk.cpp:13-46 (incl. the byte-count memcpy bug)
  *   - MERGE decompress: engine/modules/cpu_optimize.cpp:40-72
  *   - sparse SGD  : optim/sgd.cpp:34-55, 221-263 (scalar path)
+ *   - sparse Adam : optim/adam.cpp:19-86 (FMA shapes of the -O3 object code)
  *
  * The regime-B heap fill deliberately uses std::priority_queue: the
  * reference's tie order among equal block sums *is* libstdc++'s
@@ -278,6 +279,75 @@ void sgd_apply(Sgd *o, const std::string &name, float *param, uint32_t param_len
     o->iter++;
 }
 
+// ---------------------------------------------------------------------------
+// Sparse Adam (optim/adam.cpp:19-86; defaults adam.h:21-23, lr sparse_optimizer.h:30).
+// Per-name state: m, v zero-filled arrays of param_len, a float vmax (0) and a
+// uint32 tick (1), incremented after every call (adam.cpp:28-35, 81-82).
+// Arithmetic as GCC 11 -O3 -march=broadwell emits it (objdump of adam.o):
+//   b1pow = pow((double)b1, (double)tick), c1 = 1 - b1pow  (likewise b2)  :42-43,67-68
+//   maximize: g = -g; wd != 0: g = fmaf(wd, x, g)           (vfmadd231ss) :56-62
+//   mt = fmaf(b1, m, (1-b1)*g)   vt = fmaf(b2, v, ((1-b2)*g)*g)  (float)  :64-65
+//   mt_hat = (double)mt / c1     vt_hat = (double)vt / c2                  :67-68
+//   amsgrad: vmax = vt_hat > (double)vmax ? (float)vt_hat : vmax  (running over i)
+//            x' = (float)(x - lr*mt_hat / (double)(sqrtf(vmax) + eps))     :70-72
+//   else:    x' = (float)(x - lr*mt_hat / ((double)eps + sqrt(vt_hat)))    :74
+// ---------------------------------------------------------------------------
+struct Adam {
+    float lr = 1e-3f, b1 = 0.9f, b2 = 0.999f, weight_decay = 0.f, eps = 1e-8f;
+    bool amsgrad = false, maximize = false;
+    struct St {
+        std::vector<float> m, v;
+        float vmax = 0.f;
+        uint32_t tick = 1;
+    };
+    std::mutex mu;
+    std::unordered_map<std::string, St> st;
+};
+
+void adam_apply(Adam *o, const std::string &name, float *param, uint32_t param_len, const float *g_in,
+                const uint32_t *gidx, uint32_t glen) {
+    Adam::St *s;
+    {
+        std::lock_guard<std::mutex> g(o->mu);
+        auto it = o->st.find(name);
+        if (it == o->st.end()) {
+            it = o->st.emplace(name, Adam::St()).first;
+            it->second.m.assign(param_len, 0.f);
+            it->second.v.assign(param_len, 0.f);
+        }
+        s = &it->second;
+    }
+    const double c1 = 1.0 - std::pow(static_cast<double>(o->b1), static_cast<double>(s->tick));
+    const double c2 = 1.0 - std::pow(static_cast<double>(o->b2), static_cast<double>(s->tick));
+    const double lr = o->lr;
+    float vmax = s->vmax;
+    for (uint32_t i = 0; i < glen; ++i) {
+        const uint32_t id = gidx[i];
+        const float x = param[id];
+        float g = g_in[i];
+        if (o->maximize) g = -g;
+        if (o->weight_decay != 0.f) g = std::fmaf(o->weight_decay, x, g);
+        const float a = (1.f - o->b1) * g;
+        const float mt = std::fmaf(o->b1, s->m[id], a);
+        const float bq = ((1.f - o->b2) * g) * g;
+        const float vt = std::fmaf(o->b2, s->v[id], bq);
+        const double num = (static_cast<double>(mt) / c1) * lr;
+        const double vt_hat = static_cast<double>(vt) / c2;
+        double den;
+        if (o->amsgrad) {
+            if (vt_hat > static_cast<double>(vmax)) vmax = static_cast<float>(vt_hat);
+            den = static_cast<double>(std::sqrt(vmax) + o->eps);
+        } else {
+            den = static_cast<double>(o->eps) + std::sqrt(vt_hat);
+        }
+        param[id] = static_cast<float>(static_cast<double>(x) - num / den);
+        s->m[id] = mt;
+        s->v[id] = vt;
+    }
+    s->vmax = vmax;
+    s->tick++;
+}
+
 thread_local std::string g_err;
 
 }  // namespace
@@ -441,4 +511,28 @@ ORC_API int orc_sgd_momentum(void *o, const char *name, float *out, uint32_t len
     if (it == p->b.end()) return -1;
     std::memcpy(out, it->second.data(), sizeof(float) * std::min<size_t>(len, it->second.size()));
     return 0;
+}
+
+// --- sparse Adam ---
+ORC_API void *orc_adam_new(float lr, float b1, float b2, float eps, float weight_decay, int amsgrad, int maximize) {
+    auto *o = new Adam();
+    o->lr = lr; o->b1 = b1; o->b2 = b2; o->eps = eps; o->weight_decay = weight_decay;
+    o->amsgrad = amsgrad != 0; o->maximize = maximize != 0;
+    return o;
+}
+ORC_API void orc_adam_free(void *o) { delete static_cast<Adam *>(o); }
+ORC_API void orc_adam_apply(void *o, const char *name, float *param, uint32_t param_len, const float *g,
+                            const uint32_t *gidx, uint32_t glen) {
+    adam_apply(static_cast<Adam *>(o), name, param, param_len, g, gidx, glen);
+}
+ORC_API int orc_adam_state(void *o, const char *name, float *m, float *v, uint32_t len, float *vmax) {
+    auto *p = static_cast<Adam *>(o);
+    std::lock_guard<std::mutex> g(p->mu);
+    auto it = p->st.find(name);
+    if (it == p->st.end()) return -1;
+    const size_t c = std::min<size_t>(len, it->second.m.size());
+    std::memcpy(m, it->second.m.data(), sizeof(float) * c);
+    std::memcpy(v, it->second.v.data(), sizeof(float) * c);
+    *vmax = it->second.vmax;
+    return static_cast<int>(it->second.tick);
 }

@@ -19,6 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
 MANIFEST = json.load(open(os.path.join(GOLD, "manifest.json")))
 ARR = np.load(os.path.join(GOLD, "golden.npz"))
+MANIFEST_ADAM = json.load(open(os.path.join(GOLD, "manifest_adam.json")))
+ARR_ADAM = np.load(os.path.join(GOLD, "golden_adam.npz"))
 
 
 def sha(a):
@@ -89,6 +91,28 @@ def test_sgd_oracle_matches_reference(oracle, case):
         m = oracle.sgd_momentum(o, "p", n)
         np.testing.assert_array_equal(m.view(np.uint32), ARR[key].view(np.uint32))
     oracle.sgd_free(o)
+
+
+@pytest.mark.parametrize("case", MANIFEST_ADAM["adam"], ids=lambda c: c["name"])
+def test_adam_oracle_matches_reference(oracle, case):
+    """optim/adam.cpp:19-86 restated; param, m, v, vmax and tick bit-exact."""
+    n, k = case["n"], case["k"]
+    o = oracle.adam_new(case["lr"], case["b1"], case["b2"], case["eps"], case["weight_decay"], case["amsgrad"],
+                        case["maximize"])
+    h = oracle.tv16_new()
+    param = synth(n, seed_for(case["seed_bucket"], 99)) * np.float32(1000.0)
+    for s in range(case["steps"]):
+        g = synth(n, seed_for(case["seed_bucket"], s))
+        cnt, idx, val = oracle.tv16_compress(h, "p", g, k)
+        oracle.adam_apply(o, "p", param, val[:cnt], idx[:cnt])
+    name = case["name"]
+    np.testing.assert_array_equal(param.view(np.uint32), ARR_ADAM[f"{name}/param"].view(np.uint32))
+    m, v, vmax, tick = oracle.adam_state(o, "p", n)
+    np.testing.assert_array_equal(m.view(np.uint32), ARR_ADAM[f"{name}/m"].view(np.uint32))
+    np.testing.assert_array_equal(v.view(np.uint32), ARR_ADAM[f"{name}/v"].view(np.uint32))
+    assert f32bits(vmax) == case["vmax_bits"] and tick == case["tick"]
+    oracle.adam_free(o)
+    oracle.tv16_free(h)
 
 
 def test_goldens_cover_both_regimes():
