@@ -44,6 +44,7 @@ extern "C" {
 
 typedef struct stg_codec *stg_codec_t;
 typedef struct stg_sgd *stg_sgd_t;
+typedef struct stg_adam *stg_adam_t;
 
 /* Method strings as in the reference factory (core.cpp:110-118).
  * "topk" reproduces the reference's shipped behaviour (the byte-count memcpy
@@ -151,6 +152,25 @@ int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, u
                                 const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
                                 const uint32_t *d_grad_len, void *stream);
 int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_t len, void *stream);
+
+/* Sparse Adam (optim/adam.cpp:19-86; options Adam::configure adam.cpp:90-122,
+ * defaults adam.h:21-23, lr sparse_optimizer.h:30).  optimize_raw() keeps per
+ * `name` the m and v arrays (param_len floats, zeroed), the amsgrad running
+ * max vmax (a float, 0) on the device and the tick (1, +1 per call) on the
+ * host, as adam.cpp:28-35,81-82.  Indices must be unique within a call (every
+ * codec output and the MERGE union are); with amsgrad grad_len <= param_len.
+ * Calls on one name are serialised by the caller's stream (the reference holds
+ * a mutex, adam.cpp:47).  get_state copies m, v (len floats each) and vmax to
+ * the host after synchronising `stream`, and returns the next call's tick
+ * through *tick_out; STG_ERR_INVALID before the name's first call. */
+int stg_adam_create(int device, float lr, float b1, float b2, float eps, float weight_decay, int amsgrad,
+                    int maximize, stg_adam_t *out);
+int stg_adam_destroy(stg_adam_t o);
+int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param, uint32_t param_len,
+                                 const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
+                                 const uint32_t *d_grad_len, void *stream);
+int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *host_v, uint32_t len,
+                       float *host_vmax, uint32_t *tick_out, void *stream);
 
 /* Synthetic fp32 buckets from the integer-only generator of SURVEY 8(d)
  * (dist 0 = D1, 1 = D2 heavy tail, 2 = D3 zeros with prob param/1e4);

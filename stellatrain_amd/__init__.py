@@ -8,6 +8,6 @@ include/stg/codec.h.  See DESIGN.md.
 from ._capi import CodecError, lib  # noqa: F401
 from .compressor import (Compressor, ThresholdvCompressor, ThresholdvCompressor16, TopkCompressor,  # noqa: F401
                          make_compressor)
-from .engine import CodecEngine, SparseSGD, api_numel, merge_numel, owner_of, scatter_merge  # noqa: F401
+from .engine import CodecEngine, SparseAdam, SparseSGD, api_numel, merge_numel, owner_of, scatter_merge  # noqa: F401
 
 __version__ = "0.1.0"

@@ -60,6 +60,13 @@ _SIGS = {
     "stg_sgd_optimize_raw_device": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                               C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     "stg_sgd_get_momentum": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "stg_adam_create": (C.c_int, [C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int,
+                                  C.POINTER(C.c_void_p)]),
+    "stg_adam_destroy": (C.c_int, [C.c_void_p]),
+    "stg_adam_optimize_raw_device": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                               C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "stg_adam_get_state": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_void_p]),
     "stg_synth_fill_device": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_uint32, C.c_void_p]),
     "stg_last_error": (C.c_char_p, []),
 }

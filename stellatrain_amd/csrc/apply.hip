@@ -17,6 +17,17 @@
 //   momentum:  b = first ? g : fmaf(b_old, m, (1-d)*g)   (vfmadd231ss, :242)
 //   nesterov:  g = fmaf(m, b, g)  else g = b             (vfmadd231ss, :247)
 //   update:    x = (float)fma(-lr, (double)g, (double)x) (vfnmadd231sd, :256)
+//
+// Sparse Adam: optim/adam.cpp:19-86, shapes from the -O3 object code (see
+// oracle/stg_oracle.cpp adam_apply for the derivation):
+//   g = maximize ? -g : g;  wd: g = fmaf(wd, x, g)
+//   mt = fmaf(b1, m, (1-b1)*g);  vt = fmaf(b2, v, ((1-b2)*g)*g)           (float)
+//   x' = (float)(x - (mt/c1)*lr / den),  den = eps + sqrt(vt/c2)          (double)
+//   amsgrad: den = (double)(sqrtf(vmax_i) + eps), vmax_i the running max over
+//   the call's elements in stream order of (float)(vt/c2) (adam.cpp:71) -- a
+//   prefix max: per-tile maxima, one scan workgroup, then per-tile apply.
+//   Indices are unique within a call (codec output / MERGE union), so the
+//   elements are independent apart from vmax.
 #include <algorithm>
 
 #include "ws.h"
@@ -180,6 +191,148 @@ __global__ void __launch_bounds__(STG_WG) ef_zero(float *__restrict__ grad, floa
     }
 }
 
+struct AdamElem {
+    float mt, vt;
+    double num, vt_hat;
+};
+
+__device__ __forceinline__ AdamElem adam_elem(const AdamLaunch &a, float x, float g, uint32_t id) {
+    if (a.maximize) g = -g;
+    if (a.weight_decay != 0.f) g = fmaf(a.weight_decay, x, g);
+    AdamElem e;
+    e.mt = fmaf(a.b1, a.m[id], (1.f - a.b1) * g);
+    e.vt = fmaf(a.b2, a.v[id], ((1.f - a.b2) * g) * g);
+    e.num = ((double)e.mt / a.c1) * a.lr;
+    e.vt_hat = (double)e.vt / a.c2;
+    return e;
+}
+
+__device__ __forceinline__ uint32_t adam_len(const AdamLaunch &a) {
+    return a.d_grad_len ? min(a.grad_len, *a.d_grad_len) : a.grad_len;
+}
+
+__global__ void __launch_bounds__(STG_WG) adam_apply(AdamLaunch a) {
+    const uint32_t len = adam_len(a);
+    const uint32_t stride = gridDim.x * STG_WG;
+    for (uint32_t i = blockIdx.x * STG_WG + threadIdx.x; i < len; i += stride) {
+        const uint32_t id = a.gidx[i];
+        const float x = a.param[id];
+        const AdamElem e = adam_elem(a, x, a.grad[i], id);
+        a.param[id] = (float)((double)x - e.num / ((double)a.eps + sqrt(e.vt_hat)));
+        a.m[id] = e.mt;
+        a.v[id] = e.vt;
+    }
+}
+
+// amsgrad running max in the order-preserving uint map (0 = "no element": NaN
+// vt_hat never wins the reference's vt_hat > vmax test).
+__device__ __forceinline__ uint32_t ams_key(double vt_hat) {
+    return vt_hat == vt_hat ? ford((float)vt_hat) : 0u;
+}
+__device__ __forceinline__ float ams_unkey(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    const uint32_t lane = __lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v = max(v, o);
+    }
+    return v;
+}
+
+// pass 1: per-tile max of the keys (reads g, x, v; writes nothing but the tile word)
+__global__ void __launch_bounds__(STG_WG) adam_tile_max(AdamLaunch a) {
+    __shared__ uint32_t sh[STG_WAVES];
+    const uint32_t len = adam_len(a);
+    const uint32_t base = blockIdx.x * ADAM_TILE;
+    uint32_t mx = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t i = base + j * STG_WG + threadIdx.x;
+        if (i < len) {
+            const uint32_t id = a.gidx[i];
+            mx = max(mx, ams_key(adam_elem(a, a.param[id], a.grad[i], id).vt_hat));
+        }
+    }
+    mx = wave_max(mx);
+    if (__lane_id() == 0) sh[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) t = max(t, sh[w]);
+        a.tiles[blockIdx.x] = t;
+    }
+}
+
+// pass 2: one workgroup, exclusive prefix max over the tiles seeded with the
+// name's vmax; tiles[ntiles + t] = prefix before tile t; the state gets the total.
+__global__ void __launch_bounds__(STG_WG) adam_tile_scan(AdamLaunch a, uint32_t ntiles) {
+    __shared__ uint32_t sh[STG_WAVES];
+    const uint32_t len = adam_len(a);
+    const uint32_t used = (len + ADAM_TILE - 1) / ADAM_TILE;
+    uint32_t carry = ford(*a.vmax);
+    for (uint32_t b0 = 0; b0 < used; b0 += STG_WG) {
+        const uint32_t t = b0 + threadIdx.x;
+        const uint32_t v = t < used ? a.tiles[t] : 0u;
+        const uint32_t inc = wave_incl_max(v);
+        if (__lane_id() == 63) sh[threadIdx.x >> 6] = inc;
+        __syncthreads();
+        uint32_t before = carry;
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before = max(before, sh[w]);
+        const uint32_t excl = max(before, (uint32_t)__shfl_up(inc, 1, 64) * (__lane_id() != 0));
+        if (t < used) a.tiles[ntiles + t] = excl;
+        uint32_t tot = carry;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) tot = max(tot, sh[w]);
+        __syncthreads();
+        carry = tot;
+    }
+    if (threadIdx.x == 0) *a.vmax = ams_unkey(carry);
+}
+
+// pass 3: per tile, the in-tile running max combined with the tile's prefix
+__global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t ntiles) {
+    __shared__ uint32_t sh[STG_WAVES];
+    const uint32_t len = adam_len(a);
+    const uint32_t base = blockIdx.x * ADAM_TILE + threadIdx.x * 4;  // 4 consecutive elements per lane
+    if (blockIdx.x * ADAM_TILE >= len) return;
+    uint32_t id[4], key[4];
+    float x[4];
+    AdamElem e[4];
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t i = base + j;
+        key[j] = 0;
+        if (i < len) {
+            id[j] = a.gidx[i];
+            x[j] = a.param[id[j]];
+            e[j] = adam_elem(a, x[j], a.grad[i], id[j]);
+            key[j] = ams_key(e[j].vt_hat);
+        }
+        run = max(run, key[j]);
+    }
+    const uint32_t inc = wave_incl_max(run);
+    if (__lane_id() == 63) sh[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    uint32_t pre = a.tiles[ntiles + blockIdx.x];
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre = max(pre, sh[w]);
+    pre = max(pre, (uint32_t)__shfl_up(inc, 1, 64) * (__lane_id() != 0));
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t i = base + j;
+        pre = max(pre, key[j]);
+        if (i < len) {
+            const float vm = ams_unkey(pre);
+            a.param[id[j]] = (float)((double)x[j] - e[j].num / (double)(sqrtf(vm) + a.eps));
+            a.m[id[j]] = e[j].mt;
+            a.v[id[j]] = e[j].vt;
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
@@ -224,6 +377,19 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
 hipError_t launch_sgd(const SgdLaunch &a, hipStream_t s) {
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((a.grad_len + STG_WG - 1) / STG_WG, 2048));
     sgd_apply<<<blocks, STG_WG, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_adam(const AdamLaunch &a, hipStream_t s) {
+    if (!a.amsgrad) {
+        const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((a.grad_len + STG_WG - 1) / STG_WG, 2048));
+        adam_apply<<<blocks, STG_WG, 0, s>>>(a);
+        return hipGetLastError();
+    }
+    const uint32_t ntiles = std::max<uint32_t>(1, (a.grad_len + ADAM_TILE - 1) / ADAM_TILE);
+    adam_tile_max<<<ntiles, STG_WG, 0, s>>>(a);
+    adam_tile_scan<<<1, STG_WG, 0, s>>>(a, ntiles);
+    adam_apply_ams<<<ntiles, STG_WG, 0, s>>>(a, ntiles);
     return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 // handle only to look up its slot and its stream's workspace, and the launch
 // sequence of one call holds that workspace's lock so calls sharing a stream
 // cannot interleave their kernels.
+#include <cmath>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -231,6 +232,26 @@ struct stg_sgd {
     ~stg_sgd() {
         (void)hipSetDevice(device);
         for (auto &kv : mom) (void)hipFree(kv.second.first);
+    }
+};
+
+struct stg_adam {
+    int device = 0;
+    float lr, b1, b2, eps, weight_decay;
+    bool amsgrad, maximize;
+    struct Name {
+        float *m = nullptr, *v = nullptr, *vmax = nullptr;
+        uint32_t *tiles = nullptr;  // amsgrad prefix scratch, 2 words per ADAM_TILE of param_len
+        uint32_t len = 0, tick = 1;
+    };
+    std::mutex mu;
+    std::unordered_map<std::string, Name> st;
+    ~stg_adam() {
+        (void)hipSetDevice(device);
+        for (auto &kv : st) {
+            (void)hipFree(kv.second.m);
+            (void)hipFree(kv.second.tiles);
+        }
     }
 };
 
@@ -716,6 +737,101 @@ int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_
     }
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     HIP_TRY(hipMemcpy(host_out, b, std::min(len, n) * sizeof(float), hipMemcpyDeviceToHost));
+    return STG_OK;
+}
+
+int stg_adam_create(int device, float lr, float b1, float b2, float eps, float weight_decay, int amsgrad,
+                    int maximize, stg_adam_t *out) {
+    if (!out) return fail(STG_ERR_INVALID, "null argument");
+    auto o = std::make_unique<stg_adam>();
+    o->device = device;
+    o->lr = lr;
+    o->b1 = b1;
+    o->b2 = b2;
+    o->eps = eps;
+    o->weight_decay = weight_decay;
+    o->amsgrad = amsgrad != 0;
+    o->maximize = maximize != 0;
+    *out = o.release();
+    return STG_OK;
+}
+
+int stg_adam_destroy(stg_adam_t o) {
+    delete o;
+    return STG_OK;
+}
+
+int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param, uint32_t param_len,
+                                 const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
+                                 const uint32_t *d_grad_len, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    if (o->amsgrad && grad_len > param_len)
+        return fail(STG_ERR_INVALID, "amsgrad: grad_len > param_len (indices must be unique)");
+    HIP_TRY(hipSetDevice(o->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    stg::AdamLaunch a;
+    uint32_t tick;
+    {
+        std::lock_guard<std::mutex> g(o->mu);
+        auto it = o->st.find(name);
+        if (it == o->st.end()) {  // adam.cpp:28-35: zeroed m and v, vmax 0, tick 1
+            stg_adam::Name nm;
+            const size_t L = std::max<size_t>(param_len, 1);
+            // one allocation: m | v | vmax
+            HIP_TRY(hipMalloc(&nm.m, (2 * L + 1) * sizeof(float)));
+            HIP_TRY(hipMemsetAsync(nm.m, 0, (2 * L + 1) * sizeof(float), s));
+            nm.v = nm.m + L;
+            nm.vmax = nm.m + 2 * L;
+            if (o->amsgrad) {
+                const size_t nt = (L + stg::ADAM_TILE - 1) / stg::ADAM_TILE;
+                HIP_TRY(hipMalloc(&nm.tiles, 2 * nt * sizeof(uint32_t)));
+            }
+            nm.len = param_len;
+            it = o->st.emplace(name, nm).first;
+        }
+        if (it->second.len != param_len) return fail(STG_ERR_INVALID, "param_len differs from the name's first call");
+        a.m = it->second.m;
+        a.v = it->second.v;
+        a.vmax = it->second.vmax;
+        a.tiles = it->second.tiles;
+        tick = it->second.tick++;  // adam.cpp:40,82
+    }
+    a.param = d_param;
+    a.param_len = param_len;
+    a.grad = d_grad;
+    a.gidx = d_idx;
+    a.grad_len = grad_len;
+    a.d_grad_len = d_grad_len;
+    a.b1 = o->b1;
+    a.b2 = o->b2;
+    a.eps = o->eps;
+    a.weight_decay = o->weight_decay;
+    a.lr = (double)o->lr;
+    a.c1 = 1.0 - std::pow((double)o->b1, (double)tick);  // adam.cpp:42,67
+    a.c2 = 1.0 - std::pow((double)o->b2, (double)tick);  // adam.cpp:43,68
+    a.amsgrad = o->amsgrad;
+    a.maximize = o->maximize;
+    if (grad_len) HIP_TRY(stg::launch_adam(a, s));
+    return STG_OK;
+}
+
+int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *host_v, uint32_t len,
+                       float *host_vmax, uint32_t *tick_out, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    stg_adam::Name nm;
+    {
+        std::lock_guard<std::mutex> g(o->mu);
+        auto it = o->st.find(name);
+        if (it == o->st.end()) return fail(STG_ERR_INVALID, "no Adam state for this name");
+        nm = it->second;
+    }
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    const size_t c = std::min(len, nm.len);
+    if (host_m) HIP_TRY(hipMemcpy(host_m, nm.m, c * sizeof(float), hipMemcpyDeviceToHost));
+    if (host_v) HIP_TRY(hipMemcpy(host_v, nm.v, c * sizeof(float), hipMemcpyDeviceToHost));
+    if (host_vmax) HIP_TRY(hipMemcpy(host_vmax, nm.vmax, sizeof(float), hipMemcpyDeviceToHost));
+    if (tick_out) *tick_out = nm.tick;
     return STG_OK;
 }
 

@@ -195,6 +195,23 @@ struct SgdLaunch {
     bool nesterov;
 };
 hipError_t launch_sgd(const SgdLaunch &a, hipStream_t s);
+
+struct AdamLaunch {
+    float *param;
+    uint32_t param_len;
+    const float *grad;
+    const uint32_t *gidx;
+    uint32_t grad_len;          // capacity of grad/gidx (grid size)
+    const uint32_t *d_grad_len; // device count (min'd with grad_len) or null
+    float *m, *v;               // per-name moment arrays (param_len floats each)
+    float *vmax;                // per-name running max (one float on the device)
+    uint32_t *tiles;            // amsgrad scratch: 2 words per ADAM_TILE tile
+    float b1, b2, eps, weight_decay;
+    double lr, c1, c2;          // c = 1 - pow(b, tick), computed on the host (adam.cpp:42-43,67-68)
+    bool amsgrad, maximize;
+};
+constexpr uint32_t ADAM_TILE = STG_WG * 4;  // amsgrad: elements per workgroup tile
+hipError_t launch_adam(const AdamLaunch &a, hipStream_t s);
 hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
                                  hipStream_t s);
 

@@ -188,3 +188,46 @@ class SparseSGD:
         rc = lib().stg_sgd_get_momentum(self._h, name.encode(), C.c_void_p(out.ctypes.data), n,
                                         C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
         return None if rc else out
+
+
+class SparseAdam:
+    """``Adam`` sparse optimizer (optim/adam.h:10-55) on the device.  Options as
+    Adam::configure (adam.cpp:90-122; defaults adam.h:21-23, lr
+    sparse_optimizer.h:30); ``optimize_raw`` as adam.cpp:19-86."""
+
+    def __init__(self, lr: float = 1e-3, b1: float = 0.9, b2: float = 0.999, eps: float = 1e-8,
+                 weight_decay: float = 0.0, amsgrad: bool = False, maximize: bool = False, device: int = 0):
+        h = C.c_void_p()
+        check(lib().stg_adam_create(device, lr, b1, b2, eps, weight_decay, int(amsgrad), int(maximize), C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().stg_adam_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def name(self) -> str:
+        return "Adam"
+
+    def optimize_raw(self, param, name: str, grad, gidx, grad_len: int | None = None, d_grad_len=None) -> None:
+        import torch
+        n = int(grad_len if grad_len is not None else grad.numel())
+        check(lib().stg_adam_optimize_raw_device(
+            self._h, name.encode(), C.c_void_p(param.data_ptr()), param.numel(), C.c_void_p(grad.data_ptr()),
+            C.c_void_p(gidx.data_ptr()), n, C.c_void_p(d_grad_len.data_ptr()) if d_grad_len is not None else None,
+            C.c_void_p(torch.cuda.current_stream(param.device.index).cuda_stream)))
+
+    def state(self, name: str, n: int):
+        """(m, v, vmax, tick) of a name, or None before its first call."""
+        import torch
+        m, v = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        vmax, tick = C.c_float(), C.c_uint32()
+        rc = lib().stg_adam_get_state(self._h, name.encode(), C.c_void_p(m.ctypes.data), C.c_void_p(v.ctypes.data),
+                                      n, C.byref(vmax), C.byref(tick),
+                                      C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        return None if rc else (m, v, np.float32(vmax.value), int(tick.value))
