@@ -172,6 +172,22 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
 int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *host_v, uint32_t len,
                        float *host_vmax, uint32_t *tick_out, void *stream);
 
+/* Wire format of the compressed stream (engine/comm_manager.cpp:486-590).
+ * stg_wire_flag returns the flag byte queueTx would send (comm_manager.cpp:
+ * 573-590, comm_manager.h:24-25): STG_WIRE_U16_IDX when tensor_numel < 65536,
+ * STG_WIRE_F16_VAL when fp16_values (FP16_COMPRESSION, config.h:64).
+ * encode writes numel indices as uint16 (flag & 1) or uint32 and numel values
+ * as fp16 bits (flag & 2) or float; decode is the receiver's inverse
+ * (comm_manager.cpp:877-906).  Both reproduce the reference's bytes exactly,
+ * including its SIMD-block / scalar-tail differences (wire.hip).  Async. */
+#define STG_WIRE_U16_IDX 0x01
+#define STG_WIRE_F16_VAL 0x02
+int stg_wire_flag(uint64_t tensor_numel, int fp16_values);
+int stg_wire_encode_device(const uint32_t *d_idx, const float *d_val, size_t numel, int flag, void *d_idx_out,
+                           void *d_val_out, void *stream);
+int stg_wire_decode_device(const void *d_idx_in, const void *d_val_in, size_t numel, int flag, uint32_t *d_idx,
+                           float *d_val, void *stream);
+
 /* Synthetic fp32 buckets from the integer-only generator of SURVEY 8(d)
  * (dist 0 = D1, 1 = D2 heavy tail, 2 = D3 zeros with prob param/1e4);
  * bit-identical to oracle/stg_oracle.cpp:orc_synth_fill. */

@@ -142,6 +142,12 @@ class Oracle(_Codecs):
         lib.orc_adam_apply.argtypes = [C.c_void_p, C.c_char_p, _f32p, C.c_uint32, _f32p, _u32p, C.c_uint32]
         lib.orc_adam_state.restype = C.c_int
         lib.orc_adam_state.argtypes = [C.c_void_p, C.c_char_p, _f32p, _f32p, C.c_uint32, C.POINTER(C.c_float)]
+        lib.orc_wire_flag.restype = C.c_uint8
+        lib.orc_wire_flag.argtypes = [C.c_uint64, C.c_int]
+        lib.orc_wire_encode.restype = None
+        lib.orc_wire_encode.argtypes = [_u32p, _f32p, C.c_size_t, C.c_uint8, C.c_void_p, C.c_void_p]
+        lib.orc_wire_decode.restype = None
+        lib.orc_wire_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint8, _u32p, _f32p]
         lib.orc_last_error.restype = C.c_char_p
 
     def synth(self, n: int, seed: int, dist: int = 0, param: int = 0) -> np.ndarray:
@@ -200,6 +206,26 @@ class Oracle(_Codecs):
         out = np.zeros(n, np.float32)
         rc = self.lib.orc_sgd_momentum(h, name.encode(), out, n)
         return None if rc else out
+
+    def wire_flag(self, tensor_numel: int, fp16_values: bool = False) -> int:
+        return int(self.lib.orc_wire_flag(tensor_numel, int(fp16_values)))
+
+    def wire_encode(self, idx, val, flag):
+        """comm_manager.cpp queueTx casts: (idx bytes as u16/u32 array, val as u16/f32 array)."""
+        idx = np.ascontiguousarray(idx, np.uint32)
+        val = np.ascontiguousarray(val, np.float32)
+        n = idx.size
+        oi = np.zeros(n, np.uint16 if flag & 1 else np.uint32)
+        ov = np.zeros(n, np.uint16 if flag & 2 else np.float32)
+        self.lib.orc_wire_encode(idx, val, n, flag, oi.ctypes.data, ov.ctypes.data)
+        return oi, ov
+
+    def wire_decode(self, widx, wval, flag):
+        widx, wval = np.ascontiguousarray(widx), np.ascontiguousarray(wval)
+        n = widx.size
+        idx, val = np.zeros(n, np.uint32), np.zeros(n, np.float32)
+        self.lib.orc_wire_decode(widx.ctypes.data, wval.ctypes.data, n, flag, idx, val)
+        return idx, val
 
     def adam_new(self, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, weight_decay=0.0, amsgrad=False, maximize=False):
         return self.lib.orc_adam_new(lr, b1, b2, eps, weight_decay, int(amsgrad), int(maximize))

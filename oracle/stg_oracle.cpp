@@ -22,6 +22,8 @@
  *   - MERGE decompress: engine/modules/cpu_optimize.cpp:40-72
  *   - sparse SGD  : optim/sgd.cpp:34-55, 221-263 (scalar path)
  *   - sparse Adam : optim/adam.cpp:19-86 (FMA shapes of the -O3 object code)
+ *   - wire format : engine/comm_manager.cpp:486-567 (index / value casts of the
+ *                   ZeroMQ ring), flags :573-590, comm_manager.h:24-27
  *
  * The regime-B heap fill deliberately uses std::priority_queue: the
  * reference's tie order among equal block sums *is* libstdc++'s
@@ -348,6 +350,72 @@ void adam_apply(Adam *o, const std::string &name, float *param, uint32_t param_l
     s->tick++;
 }
 
+// ---------------------------------------------------------------------------
+// Wire format of the compressed stream (engine/comm_manager.cpp).  queueTx
+// (:573-590) sets COMM_FLAG_UINT16_IDX (0x01) when tensor_numel < 65536
+// (IDX_COMPRESSION 1, config.h:63) and COMM_FLAG_FP16_VAL (0x02) under
+// FP16_COMPRESSION (0 in config.h:64, i.e. compiled out as shipped).  The casts
+// run 8-wide SIMD blocks while i + 8 < length, then a scalar tail, and the two
+// halves differ (the SIMD path is what the x86 instruction defines):
+//   u32->u16 (:509-528): blocks _mm_packs_epi32 = signed saturation of the
+//            int32 to int16 (idx >= 32768 -> 0x7FFF); tail (uint16_t) truncation.
+//   u16->u32 (:486-505): blocks _mm256_cvtepi16_epi32 = SIGN extension; tail
+//            zero extension.
+//   f32->f16 (:530-548): blocks _mm256_cvtps_ph(v, 0) = IEEE binary16, round
+//            to nearest even; tail `dst[i] = src[i]` with fp16_t = uint16_t
+//            (comm_manager.h:27), i.e. GCC's vcvttss2si to int32 (truncation,
+//            out of range / NaN -> 0x80000000) stored as the low 16 bits.
+//   f16->f32 (:550-567): blocks _mm256_cvtph_ps (exact); tail the integer
+//            value of the uint16 converted to float.
+// ---------------------------------------------------------------------------
+size_t wire_simd_end(size_t len) { return len ? 8 * ((len - 1) / 8) : 0; }
+
+uint16_t f32_to_f16_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    const uint32_t sign = (u >> 16) & 0x8000u;
+    const uint32_t ex = (u >> 23) & 0xffu;
+    uint32_t man = u & 0x7fffffu;
+    if (ex == 0xffu) return static_cast<uint16_t>(sign | 0x7c00u | (man ? 0x200u | (man >> 13) : 0u));
+    const int e = static_cast<int>(ex) - 127 + 15;
+    if (e >= 31) return static_cast<uint16_t>(sign | 0x7c00u);
+    if (e <= 0) {  // binary16 subnormal (or zero)
+        if (e < -10) return static_cast<uint16_t>(sign);
+        man |= 0x800000u;
+        const uint32_t shift = static_cast<uint32_t>(14 - e);
+        uint32_t h = man >> shift;
+        const uint32_t rem = man & ((1u << shift) - 1u), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (h & 1u))) ++h;
+        return static_cast<uint16_t>(sign | h);
+    }
+    uint32_t h = (static_cast<uint32_t>(e) << 10) | (man >> 13);
+    const uint32_t rem = man & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;  // may carry into the exponent (-> inf)
+    return static_cast<uint16_t>(sign | h);
+}
+
+float f16_to_f32(uint16_t h) {
+    const uint32_t sign = static_cast<uint32_t>(h & 0x8000u) << 16;
+    uint32_t ex = (h >> 10) & 0x1fu, man = h & 0x3ffu, u;
+    if (ex == 0x1fu) u = sign | 0x7f800000u | (man << 13);
+    else if (ex) u = sign | ((ex + 112u) << 23) | (man << 13);
+    else if (!man) u = sign;
+    else {
+        int e = -1;
+        do { man <<= 1; ++e; } while (!(man & 0x400u));
+        u = sign | ((112u - static_cast<uint32_t>(e)) << 23) | ((man & 0x3ffu) << 13);
+    }
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+uint16_t f32_to_u16_trunc(float f) {  // vcvttss2si r32 + 16-bit store
+    int32_t t = INT32_MIN;
+    if (f == f && f > -2147483904.0f && f < 2147483648.0f) t = static_cast<int32_t>(f);
+    return static_cast<uint16_t>(static_cast<uint32_t>(t) & 0xffffu);
+}
+
 thread_local std::string g_err;
 
 }  // namespace
@@ -535,4 +603,49 @@ ORC_API int orc_adam_state(void *o, const char *name, float *m, float *v, uint32
     std::memcpy(v, it->second.v.data(), sizeof(float) * c);
     *vmax = it->second.vmax;
     return static_cast<int>(it->second.tick);
+}
+
+// --- wire format (engine/comm_manager.cpp) ---
+ORC_API uint8_t orc_wire_flag(uint64_t tensor_numel, int fp16_values) {
+    return static_cast<uint8_t>((tensor_numel < 65536 ? 0x01 : 0) | (fp16_values ? 0x02 : 0));
+}
+ORC_API void orc_wire_encode(const uint32_t *idx, const float *val, size_t len, uint8_t flag, void *idx_out,
+                             void *val_out) {
+    const size_t se = wire_simd_end(len);
+    for (size_t i = 0; i < len; ++i) {
+        if (flag & 0x01) {
+            uint16_t w;
+            if (i < se) {
+                const int32_t v = static_cast<int32_t>(idx[i]);
+                w = static_cast<uint16_t>(v > 32767 ? 32767 : (v < -32768 ? -32768 : v));
+            } else {
+                w = static_cast<uint16_t>(idx[i]);
+            }
+            static_cast<uint16_t *>(idx_out)[i] = w;
+        } else {
+            static_cast<uint32_t *>(idx_out)[i] = idx[i];
+        }
+        if (flag & 0x02)
+            static_cast<uint16_t *>(val_out)[i] = i < se ? f32_to_f16_rne(val[i]) : f32_to_u16_trunc(val[i]);
+        else
+            static_cast<float *>(val_out)[i] = val[i];
+    }
+}
+ORC_API void orc_wire_decode(const void *idx_in, const void *val_in, size_t len, uint8_t flag, uint32_t *idx,
+                             float *val) {
+    const size_t se = wire_simd_end(len);
+    for (size_t i = 0; i < len; ++i) {
+        if (flag & 0x01) {
+            const uint16_t w = static_cast<const uint16_t *>(idx_in)[i];
+            idx[i] = i < se ? static_cast<uint32_t>(static_cast<int32_t>(static_cast<int16_t>(w))) : w;
+        } else {
+            idx[i] = static_cast<const uint32_t *>(idx_in)[i];
+        }
+        if (flag & 0x02) {
+            const uint16_t h = static_cast<const uint16_t *>(val_in)[i];
+            val[i] = i < se ? f16_to_f32(h) : static_cast<float>(h);
+        } else {
+            val[i] = static_cast<const float *>(val_in)[i];
+        }
+    }
 }

@@ -835,6 +835,36 @@ int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *hos
     return STG_OK;
 }
 
+int stg_wire_flag(uint64_t tensor_numel, int fp16_values) {
+    return (tensor_numel < 65536 ? STG_WIRE_U16_IDX : 0) | (fp16_values ? STG_WIRE_F16_VAL : 0);
+}
+
+int stg_wire_encode_device(const uint32_t *d_idx, const float *d_val, size_t numel, int flag, void *d_idx_out,
+                           void *d_val_out, void *stream) {
+    if (flag & ~(STG_WIRE_U16_IDX | STG_WIRE_F16_VAL)) return fail(STG_ERR_INVALID, "unknown wire flag bits");
+    if (!numel) return STG_OK;
+    if (!d_idx || !d_val || !d_idx_out || !d_val_out) return fail(STG_ERR_INVALID, "null argument");
+    int dev = 0, ncu = 256;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(stg::launch_wire_encode(d_idx, d_val, numel, (uint32_t)flag, d_idx_out, d_val_out, ncu,
+                                    static_cast<hipStream_t>(stream)));
+    return STG_OK;
+}
+
+int stg_wire_decode_device(const void *d_idx_in, const void *d_val_in, size_t numel, int flag, uint32_t *d_idx,
+                           float *d_val, void *stream) {
+    if (flag & ~(STG_WIRE_U16_IDX | STG_WIRE_F16_VAL)) return fail(STG_ERR_INVALID, "unknown wire flag bits");
+    if (!numel) return STG_OK;
+    if (!d_idx_in || !d_val_in || !d_idx || !d_val) return fail(STG_ERR_INVALID, "null argument");
+    int dev = 0, ncu = 256;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(stg::launch_wire_decode(d_idx_in, d_val_in, numel, (uint32_t)flag, d_idx, d_val, ncu,
+                                    static_cast<hipStream_t>(stream)));
+    return STG_OK;
+}
+
 int stg_synth_fill_device(float *d_dst, size_t n, uint64_t seed, int dist, uint32_t param, void *stream) {
     if (!n) return STG_OK;
     HIP_TRY(stg::launch_synth(d_dst, n, seed, dist, param, static_cast<hipStream_t>(stream)));

@@ -212,6 +212,10 @@ struct AdamLaunch {
 };
 constexpr uint32_t ADAM_TILE = STG_WG * 4;  // amsgrad: elements per workgroup tile
 hipError_t launch_adam(const AdamLaunch &a, hipStream_t s);
+hipError_t launch_wire_encode(const uint32_t *idx, const float *val, size_t n, uint32_t flag, void *idx_out,
+                              void *val_out, int num_cu, hipStream_t s);
+hipError_t launch_wire_decode(const void *idx_in, const void *val_in, size_t n, uint32_t flag, uint32_t *idx,
+                              float *val, int num_cu, hipStream_t s);
 hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
                                  hipStream_t s);
 

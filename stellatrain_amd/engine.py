@@ -150,6 +150,46 @@ def scatter_merge(idx, val, per_rank: int, world: int, n: int, dense=None, mark=
     return out_idx, out_val, count
 
 
+WIRE_U16_IDX = 0x01  # COMM_FLAG_UINT16_IDX (comm_manager.h:24)
+WIRE_F16_VAL = 0x02  # COMM_FLAG_FP16_VAL (comm_manager.h:25)
+
+
+def wire_flag(tensor_numel: int, fp16_values: bool = False) -> int:
+    """The flag byte CommManager::queueTx sends (comm_manager.cpp:573-590)."""
+    return int(lib().stg_wire_flag(tensor_numel, int(fp16_values)))
+
+
+def wire_encode(idx, val, flag: int, idx_out=None, val_out=None):
+    """Pack a (idx, val) stream into the ring's wire layout on the device
+    (comm_manager.cpp:509-548): int16-typed u16 indices when ``flag & 1``,
+    fp16 bits (as int16) when ``flag & 2``; otherwise the 32-bit arrays."""
+    import torch
+    dev, n = idx.device, idx.numel()
+    if idx_out is None:
+        idx_out = torch.empty(n, dtype=torch.int16 if flag & WIRE_U16_IDX else torch.int32, device=dev)
+    if val_out is None:
+        val_out = torch.empty(n, dtype=torch.int16 if flag & WIRE_F16_VAL else torch.float32, device=dev)
+    check(lib().stg_wire_encode_device(C.c_void_p(idx.data_ptr()), C.c_void_p(val.data_ptr()), n, flag,
+                                       C.c_void_p(idx_out.data_ptr()), C.c_void_p(val_out.data_ptr()),
+                                       C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+    return idx_out, val_out
+
+
+def wire_decode(widx, wval, flag: int, idx=None, val=None):
+    """Unpack a received stream (comm_manager.cpp:877-906) into int32 indices
+    and float32 values on the device."""
+    import torch
+    dev, n = widx.device, widx.numel()
+    if idx is None:
+        idx = torch.empty(n, dtype=torch.int32, device=dev)
+    if val is None:
+        val = torch.empty(n, dtype=torch.float32, device=dev)
+    check(lib().stg_wire_decode_device(C.c_void_p(widx.data_ptr()), C.c_void_p(wval.data_ptr()), n, flag,
+                                       C.c_void_p(idx.data_ptr()), C.c_void_p(val.data_ptr()),
+                                       C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+    return idx, val
+
+
 class SparseSGD:
     """``SGD`` sparse optimizer (optim/sgd.h:10-50) on the device.  Options as
     SGD::configure (sgd.cpp:265-300); ``optimize_raw`` as sgd.cpp:34-263."""

@@ -102,3 +102,11 @@ def test_owner_of_balances_and_is_deterministic():
         assert own == owner_of(sizes, world)
         load = np.bincount(own, weights=sizes, minlength=world)
         assert load.max() - load.min() <= sizes.max()
+
+
+def test_wire_flag_matches_oracle_without_gpu(oracle):
+    """stg_wire_flag is host logic: the queueTx flag rule (comm_manager.cpp:573-590)."""
+    from stellatrain_amd import wire_flag
+    for n in (0, 1, 65535, 65536, 1 << 24):
+        for fp16 in (False, True):
+            assert wire_flag(n, fp16) == oracle.wire_flag(n, fp16)
