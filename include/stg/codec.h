@@ -99,6 +99,18 @@ typedef struct stg_bucket {
  * bucket b+1's streaming pass; a repeated key starts a new launch. */
 int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, size_t nbuckets, void *stream);
 
+/* One iteration's MERGE compress tasks with their error feedback
+ * (ModuleCompress::run, engine/modules/compress.cpp:139-186): the batched
+ * compress above, then for every bucket src[idx[i]] = 0 for i < idx_cap
+ * (:178-179; the caller zero-fills idx, compress.cpp:60-64, so unused slots
+ * zero element 0 as in the reference) and residual = src (:185), i.e.
+ * d_residuals[i] ends as the bucket with the selected entries zeroed and the
+ * bucket (d_src, written here) ends identical to it.  thresholdv16 fuses the
+ * residual copy into its streaming pass (one HBM read of the bucket instead
+ * of two); the other codecs run compress + stg_error_feedback_device. */
+int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, float *const *d_residuals,
+                                    size_t nbuckets, void *stream);
+
 /* Per-key AIMD state (thresholdv16.cpp:243-259, thresholdv.cpp:72-80), read
  * back for parity tests; synchronises `stream`.  Returns STG_ERR_INVALID when
  * the key has never been compressed.  For threshold-v pass the src pointer

@@ -100,11 +100,15 @@ class Compressor:
         if rc:
             check(rc)
 
-    def compress_batch_async(self, items, stream=None, counts=None):
+    def compress_batch_async(self, items, stream=None, counts=None, residuals=None):
         """Batched device compress (``stg_codec_compress_batch_device``): the
         same results as ``compress_async`` on each (name, src, k, dst_idx,
         dst_val[, idx_offset]) in order, on one stream.  Returns a
-        (len(items),) int32 tensor of counts (no host sync)."""
+        (len(items),) int32 tensor of counts (no host sync).  With
+        ``residuals`` (one float32 tensor per item) it is the MERGE compress
+        with error feedback (``stg_merge_compress_batch_device``,
+        compress.cpp:139-186): every src is zeroed at its dst_idx slots and its
+        residual receives the zeroed bucket."""
         import torch
         if not items:
             return None
@@ -123,7 +127,17 @@ class Compressor:
             arr[j] = StgBucket(kb, src.data_ptr(), src.numel(), int(k), di.data_ptr(), di.numel(), dv.data_ptr(),
                                dv.numel(), int(off), counts.data_ptr() + 4 * j)
         sp = stream if stream is not None else _stream_ptr(dev.index)
-        check(lib().stg_codec_compress_batch_device(self._h, arr, len(items), C.c_void_p(sp)))
+        if residuals is None:
+            check(lib().stg_codec_compress_batch_device(self._h, arr, len(items), C.c_void_p(sp)))
+            return counts
+        if len(residuals) != len(items):
+            raise ValueError("one residual per bucket")
+        rp = (C.c_void_p * len(items))()
+        for j, (it, r) in enumerate(zip(items, residuals)):
+            if r.numel() != it[1].numel() or r.dtype != torch.float32 or not r.is_contiguous() or not r.is_cuda:
+                raise ValueError("residual must be a contiguous float32 device tensor of the bucket's size")
+            rp[j] = r.data_ptr()
+        check(lib().stg_merge_compress_batch_device(self._h, arr, rp, len(items), C.c_void_p(sp)))
         return counts
 
     @staticmethod

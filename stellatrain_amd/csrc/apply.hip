@@ -335,6 +335,15 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
 
 }  // namespace
 
+hipError_t launch_ef_zero(float *grad, float *resid, const uint32_t *idx, size_t numel, size_t n, int num_cu,
+                          hipStream_t s) {
+    if (!numel) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((numel + STG_WG - 1) / STG_WG,
+                                                                          (size_t)num_cu * 4));
+    ef_zero<<<blocks, STG_WG, 0, s>>>(grad, resid, idx, numel, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
                                  hipStream_t s) {
     if (n) {

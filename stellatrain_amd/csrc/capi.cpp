@@ -377,7 +377,7 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
 // thresholdv16 over a sequence of buckets: runs of distinct keys (<= 16)
 // share one launch; the per-key state makes a repeated key wait for the
 // launch that updates it.
-int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s) {
+int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s, float *const *resid = nullptr) {
     HIP_TRY(hipSetDevice(h->device));
     Workspace *ws = nullptr;
     int rc = h->workspace(s, &ws);
@@ -409,9 +409,26 @@ int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s) {
         t.count_out = b.d_count;
         t.state = st;
         t.first = fresh;
+        t.resid = resid ? resid[i] : nullptr;
         grp.push_back(t);
     }
     return launch_tv16_group(h, ws, grp, s);
+}
+
+// ModuleCompress::run MERGE error feedback (compress.cpp:172-186) after the
+// codec: the ragged tail (not streamed by the fused kernel) is copied, then the
+// numel = idx_cap selected slots are zeroed in the bucket and the residual.
+int ef_after(stg_codec *h, const stg_bucket_t &b, float *resid, bool fused, hipStream_t s) {
+    float *g = const_cast<float *>(b.d_src);
+    if (!fused) {
+        HIP_TRY(stg::launch_error_feedback(g, b.n, b.d_idx, b.idx_cap, resid, h->num_cu, s));
+        return STG_OK;
+    }
+    const size_t full = b.n / 16 * 16;
+    if (b.n > full)
+        HIP_TRY(hipMemcpyAsync(resid + full, g + full, (b.n - full) * sizeof(float), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(stg::launch_ef_zero(g, resid, b.d_idx, b.idx_cap, b.n, h->num_cu, s));
+    return STG_OK;
 }
 
 int run_device(stg_codec *h, const char *key, const float *d_src, const void *key_ptr, size_t n, uint32_t k,
@@ -508,6 +525,35 @@ int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
                                   b.idx_offset, b.d_count, s);
         if (rc) return rc;
     }
+    return STG_OK;
+}
+
+int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, float *const *d_residuals,
+                                    size_t nbuckets, void *stream) {
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    if (nbuckets && (!buckets || !d_residuals)) return fail(STG_ERR_INVALID, "null bucket or residual array");
+    for (size_t i = 0; i < nbuckets; ++i) {
+        const stg_bucket_t &b = buckets[i];
+        const int rc = validate(h, b.n, b.k, b.idx_cap, b.val_cap, b.d_count);
+        if (rc) return rc;
+        if (b.n && !d_residuals[i]) return fail(STG_ERR_INVALID, "null residual");
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool fused = h->method == M_TV16;
+    int rc;
+    if (fused) {
+        if ((rc = run_tv16(h, buckets, nbuckets, s, d_residuals))) return rc;
+    } else {
+        for (size_t i = 0; i < nbuckets; ++i) {
+            const stg_bucket_t &b = buckets[i];
+            if ((rc = run_device(h, b.key, b.d_src, b.d_src, b.n, b.k, b.d_idx, b.idx_cap, b.d_val, b.val_cap,
+                                 b.idx_offset, b.d_count, s)))
+                return rc;
+        }
+    }
+    for (size_t i = 0; i < nbuckets; ++i)
+        if (buckets[i].n && (rc = ef_after(h, buckets[i], d_residuals[i], fused, s))) return rc;
     return STG_OK;
 }
 

@@ -166,7 +166,7 @@ struct BucketDesc {  // 80 bytes
     uint32_t nb, tl, dst_len;
     int32_t idx_offset;
     uint32_t cs, nc;  // chunks [cs, cs + nc) of the launch's chunk sequence (nc >= 1)
-    uint32_t pad[2];
+    float *resid;     // fused error feedback: the streaming waves copy every full line here (or null)
 };
 
 struct BatchArgs {
@@ -424,6 +424,19 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(d.src + (size_t)L0 * 16), 0, nl * 64u, 0x00020000);
     const uint32_t lane_line = s * 16 + (lane >> 2);
+    // fused error feedback (compress.cpp:185's memcpy(residual, src)): each
+    // streamed granule is also stored, nontemporally, to the residual; the
+    // selected entries are zeroed afterwards (ef_zero) as the reference does
+    const bool ef = d.resid != nullptr;
+    const __amdgpu_buffer_rsrc_t rsrc_r = __builtin_amdgcn_make_buffer_rsrc(
+        d.resid + (size_t)L0 * 16, 0, ef ? nl * 64u : 0u, 0x00020000);
+    auto store_r = [&](uint32_t m, float4 x) {
+        uint32_t voff = lane_line * 64u + q * 16u;
+        asm volatile("" : "+v"(voff));
+        u4v t4;
+        t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
+        __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NS * 1024u), 0, 2 /* nt */);
+    };
     auto load = [&](uint32_t m) -> float4 {
         uint32_t voff = lane_line * 64u + q * 16u;
         asm volatile("" : "+v"(voff));  // opaque: no hoisted per-step offsets
@@ -468,6 +481,7 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
                 continue;
             }
             const float S = quad_line_sum(x);  // the same in all four lanes of the quad
+            if (ef) store_r(m0 + u, x);
             v[u] = load(m0 + u + SCAN_D);
             const uint32_t us = f2u(S);
             // one test for the common case: no line of the step reaches the
@@ -1539,6 +1553,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         d.count_out = b.count_out;
         d.state = b.state;
         d.sums_g = b.sums;
+        d.resid = b.resid;
         d.nb = (uint32_t)(b.n / 16);
         d.tl = (uint32_t)(b.n % 16);
         d.dst_len = b.dst_len;

@@ -125,6 +125,7 @@ struct Tv16Bucket {
     KeyState *state;
     bool first;        // no AIMD state yet: compute the first threshold
     float *sums;       // per-bucket scratch (first threshold; ranges beyond LDS)
+    float *resid;      // MERGE error feedback: receives the bucket's full lines, or null
 };
 struct Tv16Launch {
     const Tv16Bucket *b;
@@ -216,6 +217,8 @@ hipError_t launch_wire_encode(const uint32_t *idx, const float *val, size_t n, u
                               void *val_out, int num_cu, hipStream_t s);
 hipError_t launch_wire_decode(const void *idx_in, const void *val_in, size_t n, uint32_t flag, uint32_t *idx,
                               float *val, int num_cu, hipStream_t s);
+hipError_t launch_ef_zero(float *grad, float *resid, const uint32_t *idx, size_t numel, size_t n, int num_cu,
+                          hipStream_t s);
 hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, size_t numel, float *resid, int num_cu,
                                  hipStream_t s);
 

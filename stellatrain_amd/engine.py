@@ -112,15 +112,19 @@ class CodecEngine:
         numel = merge_numel(n, self.compression_ratio_, world)
         idx = torch.zeros(numel * world, dtype=torch.int32, device=grad.device)
         val = torch.zeros(numel * world, dtype=torch.float32, device=grad.device)
-        cnt = self.compressor_.compress_async(key, grad.reshape(-1), numel, idx[:numel], val[:numel], 0)
-        if residual is not None:
-            import ctypes
-            from ._capi import check, lib
-            if residual.numel() != n or residual.dtype != torch.float32 or not residual.is_contiguous():
-                raise ValueError("residual must be a contiguous float32 tensor of the bucket's size")
-            check(lib().stg_error_feedback_device(ctypes.c_void_p(grad.data_ptr()), n, ctypes.c_void_p(idx.data_ptr()),
-                                                  numel, ctypes.c_void_p(residual.data_ptr()),
-                                                  ctypes.c_void_p(torch.cuda.current_stream(grad.device).cuda_stream)))
+        if not grad.is_contiguous():
+            raise ValueError("grad must be contiguous")
+        if residual is not None and (residual.numel() != n or residual.dtype != torch.float32
+                                     or not residual.is_contiguous()):
+            raise ValueError("residual must be a contiguous float32 tensor of the bucket's size")
+        g = grad.reshape(-1)
+        if residual is None:
+            cnt = self.compressor_.compress_async(key, g, numel, idx[:numel], val[:numel], 0)
+        else:
+            # stg_merge_compress_batch_device: codec + error feedback, the
+            # residual copy fused into thresholdv16's streaming pass
+            cnt = self.compressor_.compress_batch_async([(key, g, numel, idx[:numel], val[:numel], 0)],
+                                                        residuals=[residual.reshape(-1)])
         return idx, val, cnt
 
 

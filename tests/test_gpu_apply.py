@@ -199,3 +199,43 @@ def test_error_feedback_kernel(gpu, n, off, numel):
     torch.cuda.synchronize()
     assert torch.equal(resid, expect)
     assert torch.equal(g, expect)
+
+
+@pytest.mark.parametrize("method", ["thresholdv16", "thresholdv", "topk_exact"])
+def test_merge_compress_batch_error_feedback(gpu, oracle, method):
+    """stg_merge_compress_batch_device (compress.cpp:139-186) on a batch with
+    ragged buckets and a repeated key: the (idx, val, count) streams equal the
+    plain codec's, and every bucket and residual end as the bucket with all
+    numel selected slots zeroed.  thresholdv16 takes the fused residual copy."""
+    import torch
+    from stellatrain_amd import make_compressor
+    sizes = [(1 << 20) + 5, 65536, 100013, 4099, 262144]
+    keys = ["a@w", "b@w", "c@w", "a@w", "d@w"]  # a@w twice: the batch splits its launch
+    comp, ref = make_compressor(method), make_compressor(method)
+    keep = []  # threshold-v keys its state by src pointer: no pointer reuse across iterations
+    for it in range(2):
+        items, ritems, res, grads, srcs = [], [], [], [], []
+        for j, (n, key) in enumerate(zip(sizes, keys)):
+            src = synth(n, seed_for(60 + j, it), D2 if j % 2 else D1)
+            k = oracle.merge_numel(n, 0.99)
+            g = torch.from_numpy(src.copy()).to(gpu)
+            items.append((key, g, k, torch.zeros(k, dtype=torch.int32, device=gpu),
+                          torch.zeros(k, dtype=torch.float32, device=gpu)))
+            ritems.append((key, torch.from_numpy(src.copy()).to(gpu), k, torch.zeros(k, dtype=torch.int32, device=gpu),
+                           torch.zeros(k, dtype=torch.float32, device=gpu)))
+            res.append(torch.full((n,), 7.0, dtype=torch.float32, device=gpu))
+            grads.append(g)
+            srcs.append(src)
+        keep.append((items, ritems, res))
+        cnt = comp.compress_batch_async(items, residuals=res)
+        rcnt = ref.compress_batch_async(ritems)
+        torch.cuda.synchronize()
+        assert np.array_equal(cnt.cpu().numpy(), rcnt.cpu().numpy())
+        for j in range(len(items)):
+            ii, rv = items[j][3].cpu().numpy(), ritems[j][4].cpu().numpy()
+            assert np.array_equal(ii, ritems[j][3].cpu().numpy())
+            assert np.array_equal(items[j][4].cpu().numpy().view(np.uint32), rv.view(np.uint32))
+            expect = srcs[j].copy()
+            expect[ii.view(np.uint32)] = 0.0
+            assert np.array_equal(res[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), j
+            assert np.array_equal(grads[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), j

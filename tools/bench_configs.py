@@ -13,7 +13,10 @@ times the other configs on one GPU and prints one JSON line per measurement:
       overlapped with the codec on bucket i (two streams);
   C4  the 1024-bucket stream (256 KiB..64 MiB, log-uniform, seeded) through
       thresholdv16 batches of 16, device resident;
-  C5  compress -> MERGE decompress -> sparse SGD (momentum 0.9) on 64 MiB;
+  C5  compress -> MERGE decompress -> sparse SGD (momentum 0.9) on 64 MiB,
+      and the same with sparse Adam (plain and amsgrad) as the apply;
+  APPLY  the optimizer applies alone on a 64 MiB param (k = 167,772 pairs
+      from the codec), and WIRE encode/decode of that stream (u16 idx, fp16 val);
   E2E thresholdv16 64 MiB host-inclusive (serial and overlapped).
 
 Every device timing rotates over >= 512 MB of distinct buckets so the 256 MB
@@ -213,8 +216,17 @@ def c4_stream(torch, batches_timed):
             "launches": len(batches)}
 
 
-def c5_round_trip(torch, steps):
-    from stellatrain_amd import SparseSGD, ThresholdvCompressor16, merge_numel, scatter_merge
+def make_opt(kind):
+    from stellatrain_amd import SparseAdam, SparseSGD
+    if kind == "sgd":
+        return SparseSGD(lr=0.1, momentum=0.9), "SGD(m=0.9)"
+    if kind == "adam":
+        return SparseAdam(lr=1e-3), "Adam"
+    return SparseAdam(lr=1e-3, amsgrad=True), "Adam(amsgrad)"
+
+
+def c5_round_trip(torch, steps, kind="sgd"):
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel, scatter_merge
     from stellatrain_amd._capi import lib
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
@@ -226,7 +238,7 @@ def c5_round_trip(torch, steps):
     for i, p in enumerate(params):
         fill(lib(), p, 777 + i, st.cuda_stream)
     comp = ThresholdvCompressor16()
-    sgd = SparseSGD(lr=0.1, momentum=0.9)
+    sgd, label = make_opt(kind)
     idx = torch.zeros(k, dtype=torch.int32, device=dev)
     val = torch.zeros(k, dtype=torch.float32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -249,15 +261,64 @@ def c5_round_trip(torch, steps):
     e1.record(st)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / steps
-    alg = 4.0 * n + 8.0 * k + 16.0 * k
-    return {"config": f"C5 thresholdv16 compress + decompress + SGD(m=0.9) 64 MiB k={k}", "us_per_step": round(us, 2),
+    alg = 4.0 * n + 8.0 * k + (16.0 if kind == "sgd" else 24.0) * k
+    return {"config": f"C5 thresholdv16 compress + decompress + {label} 64 MiB k={k}", "us_per_step": round(us, 2),
             "GBps_dense_in": round(4.0 * n / us / 1e3, 1), "alg_GBps": round(alg / us / 1e3, 1)}
+
+
+def _time_loop(torch, st, fn, calls, warmup):
+    for s in range(warmup):
+        fn(s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for s in range(calls):
+        fn(s)
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / calls
+
+
+def apply_and_wire(torch, calls):
+    """Optimizer applies and wire casts alone on one codec stream of a 64 MiB
+    bucket (k = 167,772), rotating over 9 params (> 512 MB with the moments)."""
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel, wire_decode, wire_encode
+    from stellatrain_amd._capi import lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = 16 << 20
+    k = merge_numel(n, 0.99)
+    nb = 9
+    g = bufs_for(torch, lib(), dev, n, 1, st.cuda_stream, 400)[0]
+    idx = torch.zeros(k, dtype=torch.int32, device=dev)
+    val = torch.zeros(k, dtype=torch.float32, device=dev)
+    ThresholdvCompressor16().compress("a@w", g, k, idx, val)
+    params = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(nb)]
+    for i, p in enumerate(params):
+        fill(lib(), p, 900 + i, st.cuda_stream)
+    out = []
+    for kind in ("sgd", "adam", "adam_ams"):
+        opt, label = make_opt(kind)
+        us = _time_loop(torch, st, lambda s: opt.optimize_raw(params[s % nb], f"{s % nb}@w", val, idx), calls, 2 * nb)
+        alg = 8.0 * k + (16.0 if kind == "sgd" else 24.0) * k  # (idx, g) in + RMW of param and moments
+        out.append({"config": f"APPLY {label} alone, 64 MiB param, k={k}", "us_per_call": round(us, 2),
+                    "alg_GBps": round(alg / us / 1e3, 1)})
+    for flag in (1, 3):
+        wi, wv = wire_encode(idx, val, flag)
+        us_e = _time_loop(torch, st, lambda s: wire_encode(idx, val, flag, wi, wv), calls, 8)
+        ri, rv = torch.empty_like(idx), torch.empty_like(val)
+        us_d = _time_loop(torch, st, lambda s: wire_decode(wi, wv, flag, ri, rv), calls, 8)
+        wb = k * (2 + (2 if flag & 2 else 4))
+        out.append({"config": f"WIRE flag={flag} k={k}", "encode_us": round(us_e, 2), "decode_us": round(us_d, 2),
+                    "encode_alg_GBps": round((8.0 * k + wb) / us_e / 1e3, 1),
+                    "decode_alg_GBps": round((8.0 * k + wb) / us_d / 1e3, 1)})
+    return out
 
 
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
-    p.add_argument("--only", default="c2,c3,c4,c5,e2e")
+    p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply")
     a = p.parse_args()
     import torch
     from stellatrain_amd import make_compressor
@@ -273,7 +334,11 @@ def main():
     if "c4" in only:
         emit(c4_stream(torch, 3))
     if "c5" in only:
-        emit(c5_round_trip(torch, a.calls))
+        for kind in ("sgd", "adam", "adam_ams"):
+            emit(c5_round_trip(torch, a.calls, kind))
+    if "apply" in only:
+        for d in apply_and_wire(torch, a.calls):
+            emit(d)
 
 
 if __name__ == "__main__":
