@@ -315,10 +315,63 @@ def apply_and_wire(torch, calls):
     return out
 
 
+def merge_ef(torch, calls):
+    """MERGE compress + error feedback (compress.cpp:139-186) over 16 buckets of
+    64 MiB per step (2 launches of 8): the fused thresholdv16 path
+    (stg_merge_compress_batch_device) against compress + the separate
+    stg_error_feedback_device pass.  Alg. bytes per bucket: 4n read + 4n
+    residual write + 8k stream (+ the zeroing of k slots in both arrays).
+    The error feedback zeroes the bucket in place, so every step regenerates
+    the 16 buckets (a fresh gradient per iteration, as in training); the fill
+    alone is timed too and subtracted."""
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel
+    from stellatrain_amd._capi import check, lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = 16 << 20
+    k = merge_numel(n, 0.99)
+    nb = 16
+    grads = bufs_for(torch, lib(), dev, n, nb, st.cuda_stream, 500)
+    res = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(nb)]
+    idx = [torch.zeros(k, dtype=torch.int32, device=dev) for _ in range(nb)]
+    val = [torch.zeros(k, dtype=torch.float32, device=dev) for _ in range(nb)]
+    out = []
+    for fused in (True, False):
+        comp = ThresholdvCompressor16()
+        counts = torch.zeros(nb, dtype=torch.int32, device=dev)
+
+        def step(s, run=True):
+            from stellatrain_amd.synth import seed_for
+            for h in range(2):
+                sl = range(8 * h, 8 * h + 8)
+                for j in sl:
+                    fill(lib(), grads[j], seed_for(500 + j, s), st.cuda_stream)
+                if not run:
+                    continue
+                items = [(f"{j}@w", grads[j], k, idx[j], val[j]) for j in sl]
+                if fused:
+                    comp.compress_batch_async(items, counts=counts[8 * h:], residuals=[res[j] for j in sl])
+                else:
+                    comp.compress_batch_async(items, counts=counts[8 * h:])
+                    for j in sl:
+                        check(lib().stg_error_feedback_device(C.c_void_p(grads[j].data_ptr()), n,
+                                                              C.c_void_p(idx[j].data_ptr()), k,
+                                                              C.c_void_p(res[j].data_ptr()), C.c_void_p(st.cuda_stream)))
+        us_all = _time_loop(torch, st, step, calls, 4) / nb
+        us_fill = _time_loop(torch, st, lambda s: step(s, False), calls, 2) / nb
+        us = us_all - us_fill
+        alg = 8.0 * n + 8.0 * k
+        out.append({"config": f"MERGE compress + error feedback, thresholdv16 64 MiB k={k}, "
+                              f"{'fused residual copy' if fused else 'separate EF pass'}",
+                    "us_per_bucket": round(us, 2), "fill_us_per_bucket": round(us_fill, 2), "GBps_dense_in": round(4.0 * n / us / 1e3, 1),
+                    "alg_GBps": round(alg / us / 1e3, 1), "frac": round(alg / us / 1e3 / PEAK, 3)})
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
-    p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply")
+    p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply,ef")
     a = p.parse_args()
     import torch
     from stellatrain_amd import make_compressor
@@ -336,6 +389,9 @@ def main():
     if "c5" in only:
         for kind in ("sgd", "adam", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))
+    if "ef" in only:
+        for d in merge_ef(torch, max(8, a.calls // 4)):
+            emit(d)
     if "apply" in only:
         for d in apply_and_wire(torch, a.calls):
             emit(d)
