@@ -184,6 +184,19 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
 int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *host_v, uint32_t len,
                        float *host_vmax, uint32_t *tick_out, void *stream);
 
+/* Intra-node gather-add before the codec (ModuleCpuGather::run,
+ * engine/modules/cpu_gather.cpp:59-87, add_arrays misc/array_util.h:12-54).
+ * stg_gather_slice gives local rank r's slice [n*r/N, n*(r+1)/N).  add: over
+ * that slice, d_grad0 += d_residual, then += d_grads[1], ..., d_grads[N-1]
+ * (d_grads is a host array of N device pointers; [0] is ignored, it is
+ * d_grad0), in that order per element, in one pass.  Sources may be peer
+ * GPUs' buffers when P2P access is enabled (xGMI).  d_residual may be null
+ * (no residual term; differs from adding zeros only for -0.0 elements).
+ * N <= 16.  Async on `stream`. */
+int stg_gather_slice(uint64_t n, int local_rank, int num_gpus, uint64_t *start, uint64_t *end);
+int stg_gather_add_device(float *d_grad0, const float *d_residual, const float *const *d_grads, int num_gpus,
+                          uint64_t n, int local_rank, void *stream);
+
 /* Wire format of the compressed stream (engine/comm_manager.cpp:486-590).
  * stg_wire_flag returns the flag byte queueTx would send (comm_manager.cpp:
  * 573-590, comm_manager.h:24-25): STG_WIRE_U16_IDX when tensor_numel < 65536,

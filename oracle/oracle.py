@@ -148,6 +148,10 @@ class Oracle(_Codecs):
         lib.orc_wire_encode.argtypes = [_u32p, _f32p, C.c_size_t, C.c_uint8, C.c_void_p, C.c_void_p]
         lib.orc_wire_decode.restype = None
         lib.orc_wire_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint8, _u32p, _f32p]
+        lib.orc_gather_slice.restype = None
+        lib.orc_gather_slice.argtypes = [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        lib.orc_gather_add.restype = None
+        lib.orc_gather_add.argtypes = [_f32p, _f32p, C.POINTER(C.c_void_p), C.c_int, C.c_int64, C.c_int]
         lib.orc_last_error.restype = C.c_char_p
 
     def synth(self, n: int, seed: int, dist: int = 0, param: int = 0) -> np.ndarray:
@@ -226,6 +230,17 @@ class Oracle(_Codecs):
         idx, val = np.zeros(n, np.uint32), np.zeros(n, np.float32)
         self.lib.orc_wire_decode(widx.ctypes.data, wval.ctypes.data, n, flag, idx, val)
         return idx, val
+
+    def gather_slice(self, n: int, local_rank: int, num_gpus: int):
+        a, b = C.c_int64(), C.c_int64()
+        self.lib.orc_gather_slice(n, local_rank, num_gpus, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def gather_add(self, grads, resid, local_rank: int):
+        """cpu_gather.cpp:59-87 for one local rank: grads[0] (in place) +=
+        resid, grads[1], ... over the rank's slice."""
+        ptrs = (C.c_void_p * len(grads))(*[g.ctypes.data for g in grads])
+        self.lib.orc_gather_add(grads[0], resid, ptrs, len(grads), grads[0].size, local_rank)
 
     def adam_new(self, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, weight_decay=0.0, amsgrad=False, maximize=False):
         return self.lib.orc_adam_new(lr, b1, b2, eps, weight_decay, int(amsgrad), int(maximize))

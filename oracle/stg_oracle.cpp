@@ -22,6 +22,7 @@
  *   - MERGE decompress: engine/modules/cpu_optimize.cpp:40-72
  *   - sparse SGD  : optim/sgd.cpp:34-55, 221-263 (scalar path)
  *   - sparse Adam : optim/adam.cpp:19-86 (FMA shapes of the -O3 object code)
+ *   - gather-add  : engine/modules/cpu_gather.cpp:59-87 with misc/array_util.h:12-54
  *   - wire format : engine/comm_manager.cpp:486-567 (index / value casts of the
  *                   ZeroMQ ring), flags :573-590, comm_manager.h:24-27
  *
@@ -647,5 +648,23 @@ ORC_API void orc_wire_decode(const void *idx_in, const void *val_in, size_t len,
         } else {
             val[i] = static_cast<const float *>(val_in)[i];
         }
+    }
+}
+
+// --- intra-node gather-add (engine/modules/cpu_gather.cpp:59-87) ---
+// Local rank r of N owns [len*r/N, len*(r+1)/N) of grad[0] and adds, in order,
+// the residual and grad[1] .. grad[N-1] into it; add_arrays
+// (misc/array_util.h:12-54) is a plain per-element dst += src in every path.
+ORC_API void orc_gather_slice(int64_t len, int local_rank, int num_gpus, int64_t *start, int64_t *end) {
+    *start = (len * local_rank) / num_gpus;
+    *end = (len * (local_rank + 1)) / num_gpus;
+}
+ORC_API void orc_gather_add(float *grad0, const float *resid, const float *const *grads, int num_gpus, int64_t len,
+                            int local_rank) {
+    int64_t a, b;
+    orc_gather_slice(len, local_rank, num_gpus, &a, &b);
+    for (int i = 0; i < num_gpus; ++i) {
+        const float *src = i == 0 ? resid : grads[i];
+        for (int64_t j = a; j < b; ++j) grad0[j] += src[j];
     }
 }

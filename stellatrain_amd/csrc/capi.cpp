@@ -881,6 +881,37 @@ int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *hos
     return STG_OK;
 }
 
+int stg_gather_slice(uint64_t n, int local_rank, int num_gpus, uint64_t *start, uint64_t *end) {
+    if (!start || !end) return fail(STG_ERR_INVALID, "null argument");
+    if (num_gpus < 1 || local_rank < 0 || local_rank >= num_gpus) return fail(STG_ERR_INVALID, "bad rank / GPU count");
+    *start = (uint64_t)(((int64_t)n * local_rank) / num_gpus);  // cpu_gather.cpp:59-60 (int64 arithmetic)
+    *end = (uint64_t)(((int64_t)n * (local_rank + 1)) / num_gpus);
+    return STG_OK;
+}
+
+int stg_gather_add_device(float *d_grad0, const float *d_residual, const float *const *d_grads, int num_gpus,
+                          uint64_t n, int local_rank, void *stream) {
+    if (num_gpus < 1 || num_gpus > (int)stg::GATHER_MAX) return fail(STG_ERR_UNSUPPORTED, "num_gpus outside 1..16");
+    uint64_t a = 0, b = 0;
+    int rc = stg_gather_slice(n, local_rank, num_gpus, &a, &b);
+    if (rc) return rc;
+    if (a == b) return STG_OK;
+    if (!d_grad0 || (num_gpus > 1 && !d_grads)) return fail(STG_ERR_INVALID, "null argument");
+    stg::GatherArgs g{};
+    g.dst = d_grad0;
+    g.resid = d_residual;
+    g.nsrc = (uint32_t)num_gpus;
+    for (int i = 1; i < num_gpus; ++i) {
+        if (!d_grads[i]) return fail(STG_ERR_INVALID, "null source");
+        g.src[i] = d_grads[i];
+    }
+    int dev = 0, ncu = 256;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(stg::launch_gather_add(g, a, b, ncu, static_cast<hipStream_t>(stream)));
+    return STG_OK;
+}
+
 int stg_wire_flag(uint64_t tensor_numel, int fp16_values) {
     return (tensor_numel < 65536 ? STG_WIRE_U16_IDX : 0) | (fp16_values ? STG_WIRE_F16_VAL : 0);
 }

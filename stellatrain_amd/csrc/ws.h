@@ -213,6 +213,14 @@ struct AdamLaunch {
 };
 constexpr uint32_t ADAM_TILE = STG_WG * 4;  // amsgrad: elements per workgroup tile
 hipError_t launch_adam(const AdamLaunch &a, hipStream_t s);
+constexpr uint32_t GATHER_MAX = 16;  // local GPUs per node the gather-add accepts
+struct GatherArgs {
+    float *dst;                    // grad[0]
+    const float *resid;            // residual (or null: no residual term)
+    const float *src[GATHER_MAX];  // src[1 .. nsrc-1] = grad[1 .. N-1]; src[0] unused
+    uint32_t nsrc;                 // N, the node's GPU count
+};
+hipError_t launch_gather_add(const GatherArgs &a, size_t start, size_t end, int num_cu, hipStream_t s);
 hipError_t launch_wire_encode(const uint32_t *idx, const float *val, size_t n, uint32_t flag, void *idx_out,
                               void *val_out, int num_cu, hipStream_t s);
 hipError_t launch_wire_decode(const void *idx_in, const void *val_in, size_t n, uint32_t flag, uint32_t *idx,

@@ -154,6 +154,31 @@ def scatter_merge(idx, val, per_rank: int, world: int, n: int, dense=None, mark=
     return out_idx, out_val, count
 
 
+def gather_slice(n: int, local_rank: int, num_gpus: int):
+    """Local rank's slice [n*r/N, n*(r+1)/N) of the gather-add (cpu_gather.cpp:59-61)."""
+    a, b = C.c_uint64(), C.c_uint64()
+    check(lib().stg_gather_slice(n, local_rank, num_gpus, C.byref(a), C.byref(b)))
+    return a.value, b.value
+
+
+def gather_add(grads, residual, local_rank: int) -> None:
+    """ModuleCpuGather::run on the device (cpu_gather.cpp:59-87): over this
+    local rank's slice, ``grads[0] += residual + grads[1] + ... + grads[N-1]``
+    left to right, in one pass.  ``grads`` are float32 device tensors of one
+    size (peers' buffers where P2P is enabled); ``residual`` may be None."""
+    import torch
+    g0 = grads[0]
+    n = g0.numel()
+    for t in list(grads) + ([residual] if residual is not None else []):
+        if t.numel() != n or t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("gather_add: contiguous float32 device tensors of one size")
+    ptrs = (C.c_void_p * len(grads))(*[t.data_ptr() for t in grads])
+    check(lib().stg_gather_add_device(C.c_void_p(g0.data_ptr()),
+                                      C.c_void_p(residual.data_ptr()) if residual is not None else None,
+                                      ptrs, len(grads), n, local_rank,
+                                      C.c_void_p(torch.cuda.current_stream(g0.device.index).cuda_stream)))
+
+
 WIRE_U16_IDX = 0x01  # COMM_FLAG_UINT16_IDX (comm_manager.h:24)
 WIRE_F16_VAL = 0x02  # COMM_FLAG_FP16_VAL (comm_manager.h:25)
 

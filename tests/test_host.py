@@ -110,3 +110,12 @@ def test_wire_flag_matches_oracle_without_gpu(oracle):
     for n in (0, 1, 65535, 65536, 1 << 24):
         for fp16 in (False, True):
             assert wire_flag(n, fp16) == oracle.wire_flag(n, fp16)
+
+
+def test_gather_slice_matches_oracle_without_gpu(oracle):
+    """stg_gather_slice is host logic (cpu_gather.cpp:59-61)."""
+    from stellatrain_amd import gather_slice
+    for n in (0, 1, 33, 100013, (1 << 31) + 7):
+        for g in (1, 3, 8):
+            for r in range(g):
+                assert gather_slice(n, r, g) == oracle.gather_slice(n, r, g)

@@ -124,3 +124,32 @@ def test_goldens_cover_both_regimes():
         ups += int((d > 0).sum())
         downs += int((d < 0).sum())
     assert ups > 10 and downs > 10
+
+
+MANIFEST_GATHER = json.load(open(os.path.join(GOLD, "manifest_gather.json")))
+
+
+@pytest.mark.parametrize("case", MANIFEST_GATHER["gather"], ids=lambda c: c["name"])
+def test_gather_add_oracle_matches_reference(oracle, case):
+    """cpu_gather.cpp:59-87 + array_util.h add_arrays, every local rank's slice."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden_gather import inputs
+    n, g = case["n"], case["num_gpus"]
+    grads, resid = inputs(n, g)
+    for r in range(g):
+        oracle.gather_add(grads, resid, r)
+    ref = np.load(os.path.join(GOLD, "golden_gather.npz"))[f"{case['name']}/grad0"]
+    np.testing.assert_array_equal(grads[0].view(np.uint32), ref.view(np.uint32))
+
+
+def test_gather_slices_partition(oracle):
+    """The local ranks' slices tile [0, n) exactly (cpu_gather.cpp:59-61)."""
+    for n in (0, 1, 7, 33, 100013, 1 << 24):
+        for g in range(1, 9):
+            cur = 0
+            for r in range(g):
+                a, b = oracle.gather_slice(n, r, g)
+                assert a == cur and b >= a
+                cur = b
+            assert cur == n

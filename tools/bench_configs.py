@@ -368,10 +368,35 @@ def merge_ef(torch, calls):
     return out
 
 
+def gather(torch, calls):
+    """Intra-node gather-add (cpu_gather.cpp:59-87) of a 64 MiB bucket from N
+    device-local sources (all N ranks' slices in sequence = the whole bucket).
+    Alg. bytes: 4n (dst) + 4n (residual) + 4n (N - 1) read + 4n written."""
+    from stellatrain_amd import gather_add
+    from stellatrain_amd._capi import lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = 16 << 20
+    out = []
+    for g in (2, 4, 8):
+        srcs = bufs_for(torch, lib(), dev, n, g + 1, st.cuda_stream, 600)
+        grads, resid = srcs[:g], srcs[g]
+
+        def step(s):
+            for r in range(g):
+                gather_add(grads, resid, r)
+        us = _time_loop(torch, st, step, calls, 2)
+        alg = 4.0 * n * (g + 2)
+        out.append({"config": f"GATHER-ADD 64 MiB bucket, N={g} sources + residual", "us_per_bucket": round(us, 2),
+                    "alg_GBps": round(alg / us / 1e3, 1), "frac": round(alg / us / 1e3 / PEAK, 3)})
+        del srcs, grads, resid
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
-    p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply,ef")
+    p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply,ef,gather")
     a = p.parse_args()
     import torch
     from stellatrain_amd import make_compressor
@@ -389,6 +414,9 @@ def main():
     if "c5" in only:
         for kind in ("sgd", "adam", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))
+    if "gather" in only:
+        for d in gather(torch, a.calls):
+            emit(d)
     if "ef" in only:
         for d in merge_ef(torch, max(8, a.calls // 4)):
             emit(d)

@@ -50,6 +50,7 @@ for s in "$@"; do
         c5) step c5 300 python tools/bench_configs.py --only c5 ;;
         apply) step apply 300 python tools/bench_configs.py --only c5,apply ;;
         ef) step ef 300 python tools/bench_configs.py --only ef ;;
+        gather) step gather 300 python tools/bench_configs.py --only gather ;;
         prof_apply) step prof_apply 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_apply" -o run \
                 -- python3 tools/bench_configs.py --only apply ;;
         depths)  # tuning variants built as stellatrain_amd/libstg_codec_d*.so
