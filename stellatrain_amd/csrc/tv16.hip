@@ -391,7 +391,7 @@ constexpr uint32_t DEC_B = 1, DEC_WIN = 2, DEC_TAIL = 4;
 // scan of slot j = chunk k by streaming wave s: lines i = (s + NS*m)*16 +
 // lane/4 of the chunk, m = 0, 1, ...; SCAN_D float4 loads per lane in flight
 // through a buffer descriptor bounded to the chunk (lanes past it read zeros).
-template <int STAGE>
+template <int STAGE, bool EF>
 __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint32_t s) {
     Lds &L = C.L;
     const uint32_t par = j % NBUF;
@@ -427,9 +427,9 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     // fused error feedback (compress.cpp:185's memcpy(residual, src)): each
     // streamed granule is also stored, nontemporally, to the residual; the
     // selected entries are zeroed afterwards (ef_zero) as the reference does
-    const bool ef = d.resid != nullptr;
+    // (EF: a separate instantiation, so the plain codec carries none of it)
     const __amdgpu_buffer_rsrc_t rsrc_r = __builtin_amdgcn_make_buffer_rsrc(
-        d.resid + (size_t)L0 * 16, 0, ef ? nl * 64u : 0u, 0x00020000);
+        EF ? d.resid + (size_t)L0 * 16 : nullptr, 0, (EF && d.resid) ? nl * 64u : 0u, 0x00020000);
     auto store_r = [&](uint32_t m, float4 x) {
         uint32_t voff = lane_line * 64u + q * 16u;
         asm volatile("" : "+v"(voff));
@@ -481,7 +481,7 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
                 continue;
             }
             const float S = quad_line_sum(x);  // the same in all four lanes of the quad
-            if (ef) store_r(m0 + u, x);
+            if (EF) store_r(m0 + u, x);
             v[u] = load(m0 + u + SCAN_D);
             const uint32_t us = f2u(S);
             // one test for the common case: no line of the step reaches the
@@ -1450,7 +1450,7 @@ __device__ __forceinline__ void rank_bucket(Ctx &C, uint32_t b) {
 // streaming waves' work only (the finisher releases buffers at once);
 // 3 = plain streaming read (calibration); 4 = full codec + s_memrealtime
 // stamps (tools/stamps.py); 5 = full codec without the regime-B heap fill.
-template <int STAGE>
+template <int STAGE, bool EF>
 __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
     __shared__ Lds L;
     Ctx C{A, L, gridDim.x, blockIdx.x, 0, A.ctl, A.cand, A.fail, STAGE == 4};
@@ -1495,7 +1495,7 @@ __global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
             if (k >= A.K) break;
             asm volatile("" : "+s"(C.w), "+s"(C.G));
-            scan_chunk<STAGE>(C, j, k, wave);
+            scan_chunk<STAGE, EF>(C, j, k, wave);
         }
     } else if (wave == FIN) {
         if (STG_TV16_PRIO) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
@@ -1563,6 +1563,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         K += d.nc;
     }
     if (K > a.desc_cap) return hipErrorInvalidValue;
+    bool ef = false;  // any bucket with a residual: the fused error-feedback instantiation
+    for (uint32_t i = 0; i < a.nb; ++i) ef |= a.b[i].resid != nullptr;
     A.nbk = a.nb;
     A.epoch = a.epoch;
     A.K = K;
@@ -1578,11 +1580,14 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     switch (dbg_stage) {
-        case 1: tv16_batch<1><<<G, FWG, 0, s>>>(A); break;
-        case 3: tv16_batch<3><<<G, FWG, 0, s>>>(A); break;
-        case 4: tv16_batch<4><<<G, FWG, 0, s>>>(A); break;
-        case 5: tv16_batch<5><<<G, FWG, 0, s>>>(A); break;
-        default: tv16_batch<0><<<G, FWG, 0, s>>>(A); break;
+        case 1: tv16_batch<1, false><<<G, FWG, 0, s>>>(A); break;
+        case 3: tv16_batch<3, false><<<G, FWG, 0, s>>>(A); break;
+        case 4: tv16_batch<4, false><<<G, FWG, 0, s>>>(A); break;
+        case 5: tv16_batch<5, false><<<G, FWG, 0, s>>>(A); break;
+        default:
+            if (ef) tv16_batch<0, true><<<G, FWG, 0, s>>>(A);
+            else tv16_batch<0, false><<<G, FWG, 0, s>>>(A);
+            break;
     }
     if (a.ev) {
         (void)hipEventRecord(a.ev[1], s);
