@@ -9,90 +9,90 @@
 // Three histogram levels over the 31 magnitude bits (11 + 11 + 9 bits).  Each
 // level is one streaming pass: an LDS histogram per workgroup in four copies
 // (lane & 3 picks the copy, so lanes whose keys share a bin -- magnitudes
-// cluster in a few exponents -- rarely hit one LDS address together), one
-// global atomic per non-empty bin, and the last workgroup to finish picks the
-// bin holding the rank (no separate launch).
+// cluster in a few exponents -- rarely hit one LDS address together) and one
+// global atomic per non-empty bin; then one 1024-thread workgroup picks the
+// bin holding the rank and zeroes the table.
 #include "ws.h"
 
 namespace stg {
 
 namespace {
 
-#ifndef STG_RS_LASTBLOCK
-#define STG_RS_LASTBLOCK 0  // 1: the last histogram workgroup picks; 0: one 64-thread pick launch per level
-#endif
 #ifndef STG_RS_NCOPY
 #define STG_RS_NCOPY 4
 #endif
 constexpr uint32_t NCOPY = STG_RS_NCOPY;
 constexpr uint32_t HWG = 1024;  // rs_hist workgroup: one fat workgroup per CU, few global bin atomics
+constexpr uint32_t PWG = 1024;  // rs_pick workgroup: two bins per thread at 11 bits
 
-__global__ void __launch_bounds__(STG_WG) rs_init(RSel *st, const uint32_t *d_rank, uint32_t rank) {
-    for (uint32_t i = threadIdx.x; i < RS_BINS; i += STG_WG) st->hist[i] = 0;
-    if (threadIdx.x == 0) {
-        st->prefix = 0;
-        st->mask = 0;
-        st->rank = d_rank ? *d_rank : rank;
-        st->cnt_gt = 0;
-        st->done = 0;
-    }
-}
-
-// The bin holding st->rank, counting from the top bin; run by one wave of the
-// level's last workgroup (every other workgroup's bin atomics are complete).
+// The bin holding the rank, counting from the top bin, by one 1024-thread
+// workgroup: each thread sums its (top-down) bins, a workgroup scan finds the
+// thread whose range holds the rank, that thread walks its bins.  It also
+// zeroes the histogram for the next level (and the next select: the table is
+// zero at allocation and after every complete select, so no init launch).
+// The first level (SHIFT + NBITS == 31) takes the rank from the arguments and
+// starts the prefix afresh.
 template <int SHIFT, int NBITS>
-__device__ __forceinline__ void pick(RSel *st, uint64_t extra_zeros) {
+__global__ void __launch_bounds__(PWG) rs_pick(RSel *st, uint64_t extra_zeros, const uint32_t *d_rank,
+                                              uint32_t rank_arg) {
+    constexpr bool FIRST = SHIFT + NBITS == 31;
     constexpr uint32_t NB = 1u << NBITS;
-    constexpr uint32_t PER = NB / 64;  // bins per lane, lane l owns top-down bins [PER l, PER l + PER)
-    const uint32_t lane = __lane_id();
-    const uint32_t prefix = st->prefix;
-    const uint32_t rank = st->rank;
-    uint32_t sum = 0;
+    constexpr uint32_t PER = (NB + PWG - 1) / PWG;
+    __shared__ uint32_t wsum[PWG / 64];
+    __shared__ uint32_t s_bin, s_before;
+    const uint32_t t = threadIdx.x, lane = __lane_id(), wave = t >> 6;
+    const uint32_t prefix = FIRST ? 0u : st->prefix;
+    const uint32_t rank = FIRST ? (d_rank ? *d_rank : rank_arg) : st->rank;
+    uint32_t c[PER], sum = 0;
+#pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t b = NB - 1 - (PER * lane + j);
-        uint32_t c = ld_acq_relaxed(&st->hist[b]);
-        if (b == 0 && prefix == 0) c += (uint32_t)extra_zeros;  // implicit zero keys
-        sum += c;
+        const uint32_t td = PER * t + j;  // top-down bin index
+        c[j] = 0;
+        if (td < NB) {
+            const uint32_t b = NB - 1 - td;
+            c[j] = st->hist[b];
+            if (b == 0 && prefix == 0) c[j] += (uint32_t)extra_zeros;  // implicit zero keys
+        }
+        sum += c[j];
     }
     const uint32_t incl = wave_incl_scan(sum);
-    const uint32_t before = incl - sum;
-    const uint64_t hit = __ballot(rank >= before && rank < incl);
-    uint32_t bin = 0xffffffffu, bbefore = 0;
-    if (hit) {
-        const uint32_t src = (uint32_t)__ffsll((long long)hit) - 1u;
-        if (lane == src) {
-            uint32_t acc = before;
-            for (uint32_t j = 0; j < PER; ++j) {
-                const uint32_t b = NB - 1 - (PER * lane + j);
-                uint32_t c = ld_acq_relaxed(&st->hist[b]);
-                if (b == 0 && prefix == 0) c += (uint32_t)extra_zeros;
-                if (rank < acc + c) { bin = b; bbefore = acc; break; }
-                acc += c;
-            }
+    if (lane == 63) wsum[wave] = incl;
+    if (t == 0) { s_bin = 0xffffffffu; s_before = 0; }
+    __syncthreads();
+    uint32_t before = incl - sum;
+    for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
+    if (sum && rank >= before && rank - before < sum) {
+        uint32_t acc = before;
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) {
+            if (rank - acc < c[j]) { s_bin = NB - 1 - (PER * t + j); s_before = acc; break; }
+            acc += c[j];
         }
-        bin = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)src);
-        bbefore = (uint32_t)__builtin_amdgcn_readlane((int)bbefore, (int)src);
     }
-    for (uint32_t i = lane; i < RS_BINS; i += 64) st->hist[i] = 0;  // for the next level
-    if (lane == 0) {
-        const uint32_t b = bin == 0xffffffffu ? 0 : bin;  // rank out of range: degenerate
-        st->rank = rank - bbefore;
-        st->cnt_gt += bbefore;
+    __syncthreads();
+    for (uint32_t i = t; i < RS_BINS; i += PWG) st->hist[i] = 0;
+    if (t == 0) {
+        const bool hit = s_bin != 0xffffffffu;
+        const uint32_t b = hit ? s_bin : 0u;  // rank out of range: degenerate
+        const uint32_t bb = hit ? s_before : 0u;
+        st->rank = rank - bb;
+        st->cnt_gt = (FIRST ? 0u : st->cnt_gt) + bb;
         st->prefix = prefix | (b << SHIFT);
-        st->mask |= (NB - 1) << SHIFT;
-        st->done = 0;
+        st->mask = (FIRST ? 0u : st->mask) | ((NB - 1) << SHIFT);
     }
 }
 
 template <int SHIFT, int NBITS>
 __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size_t m, uint32_t last_mask,
                                                RSel *st, uint64_t extra_zeros) {
+    constexpr bool FIRST = SHIFT + NBITS == 31;
     constexpr uint32_t NB = 1u << NBITS;
     __shared__ uint32_t h[NCOPY][NB];
-    __shared__ uint32_t s_last;
     for (uint32_t i = threadIdx.x; i < NCOPY * NB; i += HWG) (&h[0][0])[i] = 0;
-    const uint32_t prefix = st->prefix;
-    const uint32_t mask = st->mask;
+    // the first level counts every key (its prefix and mask are still those of
+    // the previous select)
+    const uint32_t prefix = FIRST ? 0u : st->prefix;
+    const uint32_t mask = FIRST ? 0u : st->mask;
     __syncthreads();
 
     uint32_t *hc = h[threadIdx.x & (NCOPY - 1)];
@@ -135,23 +135,6 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
         for (uint32_t q = 0; q < NCOPY; ++q) c += h[q][i];
         if (c) atomicAdd(&st->hist[i], c);
     }
-    // The last workgroup to finish picks the bin.  Agent-scope atomics are
-    // coherent across the XCDs without fences (an agent-scope release fence
-    // would write back the whole L2): every thread waits for its atomics to
-    // complete, then one relaxed atomic counts the workgroup done; the picker
-    // reads the bins with agent-scope loads.
-    if (!STG_RS_LASTBLOCK) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(&st->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    __syncthreads();
-    if (s_last && threadIdx.x < 64) pick<SHIFT, NBITS>(st, extra_zeros);
-}
-
-template <int SHIFT, int NBITS>
-__global__ void __launch_bounds__(64) rs_pick(RSel *st, uint64_t extra_zeros) {
-    pick<SHIFT, NBITS>(st, extra_zeros);
 }
 
 }  // namespace
@@ -161,13 +144,12 @@ hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uin
                                hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
     const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * 2));
-    rs_init<<<1, STG_WG, 0, s>>>(ws.rsel, d_rank, rank);
     rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
-    if (!STG_RS_LASTBLOCK) rs_pick<20, 11><<<1, 64, 0, s>>>(ws.rsel, extra_zeros);
+    rs_pick<20, 11><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
     rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
-    if (!STG_RS_LASTBLOCK) rs_pick<9, 11><<<1, 64, 0, s>>>(ws.rsel, extra_zeros);
+    rs_pick<9, 11><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
     rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
-    if (!STG_RS_LASTBLOCK) rs_pick<0, 9><<<1, 64, 0, s>>>(ws.rsel, extra_zeros);
+    rs_pick<0, 9><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
     return hipGetLastError();
 }
 
