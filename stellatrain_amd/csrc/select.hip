@@ -18,6 +18,9 @@ namespace stg {
 
 namespace {
 
+#ifndef STG_RS_GRIDMUL
+#define STG_RS_GRIDMUL 1  // histogram workgroups per CU (fewer global bin atomics; 2: +7 us on top-k)
+#endif
 #ifndef STG_RS_NCOPY
 #define STG_RS_NCOPY 4
 #endif
@@ -143,7 +146,7 @@ hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uin
                                const uint32_t *d_rank, uint32_t rank, const DevWS &ws, int num_cu,
                                hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
-    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * 2));
+    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
     rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
     rs_pick<20, 11><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
     rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
