@@ -25,7 +25,9 @@
 //   x' = (float)(x - (mt/c1)*lr / den),  den = eps + sqrt(vt/c2)          (double)
 //   amsgrad: den = (double)(sqrtf(vmax_i) + eps), vmax_i the running max over
 //   the call's elements in stream order of (float)(vt/c2) (adam.cpp:71) -- a
-//   prefix max: per-tile maxima, one scan workgroup, then per-tile apply.
+//   prefix max: one launch, each 1,024-element tile publishes its maximum as a
+//   tagged word and takes the maximum over its predecessors' words
+//   (decoupled look-back; max needs no inclusive chain), then applies.
 //   Indices are unique within a call (codec output / MERGE union), so the
 //   elements are independent apart from vmax.
 #include <algorithm>
@@ -243,61 +245,23 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     return v;
 }
 
-// pass 1: per-tile max of the keys (reads g, x, v; writes nothing but the tile word)
-__global__ void __launch_bounds__(STG_WG) adam_tile_max(AdamLaunch a) {
+// One launch.  Tile t (ADAM_TILE consecutive elements of the call, lane l
+// holds 4 consecutive ones) computes its elements, publishes its maximum key
+// as (tag << 32 | key) in tiles[t] -- tag = the name's tick, so words of
+// earlier calls never match -- and then reads tiles[0..t-1]: the running vmax
+// before the tile is the maximum of the name's vmax and those words (max is
+// idempotent, so no inclusive prefix chain is needed).  Predecessors have
+// lower block ids, so they are dispatched first and always finish publishing;
+// the poll is still bounded.  The last tile stores the call's vmax.
+__global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t tag) {
     __shared__ uint32_t sh[STG_WAVES];
+    __shared__ uint32_t s_pre;
     const uint32_t len = adam_len(a);
-    const uint32_t base = blockIdx.x * ADAM_TILE;
-    uint32_t mx = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        const uint32_t i = base + j * STG_WG + threadIdx.x;
-        if (i < len) {
-            const uint32_t id = a.gidx[i];
-            mx = max(mx, ams_key(adam_elem(a, a.param[id], a.grad[i], id).vt_hat));
-        }
-    }
-    mx = wave_max(mx);
-    if (__lane_id() == 0) sh[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t w = 0; w < STG_WAVES; ++w) t = max(t, sh[w]);
-        a.tiles[blockIdx.x] = t;
-    }
-}
-
-// pass 2: one workgroup, exclusive prefix max over the tiles seeded with the
-// name's vmax; tiles[ntiles + t] = prefix before tile t; the state gets the total.
-__global__ void __launch_bounds__(STG_WG) adam_tile_scan(AdamLaunch a, uint32_t ntiles) {
-    __shared__ uint32_t sh[STG_WAVES];
-    const uint32_t len = adam_len(a);
-    const uint32_t used = (len + ADAM_TILE - 1) / ADAM_TILE;
-    uint32_t carry = ford(*a.vmax);
-    for (uint32_t b0 = 0; b0 < used; b0 += STG_WG) {
-        const uint32_t t = b0 + threadIdx.x;
-        const uint32_t v = t < used ? a.tiles[t] : 0u;
-        const uint32_t inc = wave_incl_max(v);
-        if (__lane_id() == 63) sh[threadIdx.x >> 6] = inc;
-        __syncthreads();
-        uint32_t before = carry;
-        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before = max(before, sh[w]);
-        const uint32_t excl = max(before, (uint32_t)__shfl_up(inc, 1, 64) * (__lane_id() != 0));
-        if (t < used) a.tiles[ntiles + t] = excl;
-        uint32_t tot = carry;
-        for (uint32_t w = 0; w < STG_WAVES; ++w) tot = max(tot, sh[w]);
-        __syncthreads();
-        carry = tot;
-    }
-    if (threadIdx.x == 0) *a.vmax = ams_unkey(carry);
-}
-
-// pass 3: per tile, the in-tile running max combined with the tile's prefix
-__global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t ntiles) {
-    __shared__ uint32_t sh[STG_WAVES];
-    const uint32_t len = adam_len(a);
-    const uint32_t base = blockIdx.x * ADAM_TILE + threadIdx.x * 4;  // 4 consecutive elements per lane
-    if (blockIdx.x * ADAM_TILE >= len) return;
+    const uint32_t ntile = (len + ADAM_TILE - 1) / ADAM_TILE;
+    const uint32_t tile = blockIdx.x;
+    if (tile >= ntile) return;
+    const uint32_t base = tile * ADAM_TILE + threadIdx.x * 4;
+    const uint32_t vmax0 = ford(*a.vmax);  // read before publishing: the last tile rewrites it
     uint32_t id[4], key[4];
     float x[4];
     AdamElem e[4];
@@ -306,6 +270,9 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
     for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t i = base + j;
         key[j] = 0;
+        id[j] = 0;
+        x[j] = 0.f;
+        e[j] = AdamElem{0.f, 0.f, 0.0, 0.0};
         if (i < len) {
             id[j] = a.gidx[i];
             x[j] = a.param[id[j]];
@@ -317,7 +284,29 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
     const uint32_t inc = wave_incl_max(run);
     if (__lane_id() == 63) sh[threadIdx.x >> 6] = inc;
     __syncthreads();
-    uint32_t pre = a.tiles[ntiles + blockIdx.x];
+    uint32_t tile_max = 0;
+    for (uint32_t w = 0; w < STG_WAVES; ++w) tile_max = max(tile_max, sh[w]);
+    uint64_t *words = reinterpret_cast<uint64_t *>(a.tiles);
+    if (threadIdx.x == 0) st_sc1(&words[tile], ((uint64_t)tag << 32) | tile_max);
+    // look-back by wave 0: 64 predecessors per round
+    if (threadIdx.x < 64) {
+        uint32_t pre = vmax0;
+        for (uint32_t p0 = 0; p0 < tile; p0 += 64) {
+            const uint32_t p = p0 + threadIdx.x;
+            if (p < tile) {
+                uint64_t w = ld_sc1(&words[p]);
+                for (uint32_t spins = 0; (uint32_t)(w >> 32) != tag && spins < (1u << 22); ++spins) {
+                    __builtin_amdgcn_s_sleep(1);
+                    w = ld_sc1(&words[p]);
+                }
+                pre = max(pre, (uint32_t)w);
+            }
+        }
+        pre = wave_max(pre);
+        if (threadIdx.x == 0) s_pre = pre;
+    }
+    __syncthreads();
+    uint32_t pre = s_pre;
     for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre = max(pre, sh[w]);
     pre = max(pre, (uint32_t)__shfl_up(inc, 1, 64) * (__lane_id() != 0));
 #pragma unroll
@@ -331,6 +320,7 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
             a.v[id[j]] = e[j].vt;
         }
     }
+    if (tile == ntile - 1 && threadIdx.x == STG_WG - 1) *a.vmax = ams_unkey(pre);
 }
 
 }  // namespace
@@ -396,9 +386,7 @@ hipError_t launch_adam(const AdamLaunch &a, hipStream_t s) {
         return hipGetLastError();
     }
     const uint32_t ntiles = std::max<uint32_t>(1, (a.grad_len + ADAM_TILE - 1) / ADAM_TILE);
-    adam_tile_max<<<ntiles, STG_WG, 0, s>>>(a);
-    adam_tile_scan<<<1, STG_WG, 0, s>>>(a, ntiles);
-    adam_apply_ams<<<ntiles, STG_WG, 0, s>>>(a, ntiles);
+    adam_apply_ams<<<ntiles, STG_WG, 0, s>>>(a, a.tag);
     return hipGetLastError();
 }
 

@@ -241,7 +241,7 @@ struct stg_adam {
     bool amsgrad, maximize;
     struct Name {
         float *m = nullptr, *v = nullptr, *vmax = nullptr;
-        uint32_t *tiles = nullptr;  // amsgrad prefix scratch, 2 words per ADAM_TILE of param_len
+        uint32_t *tiles = nullptr;  // amsgrad look-back words, one uint64 per ADAM_TILE of param_len
         uint32_t len = 0, tick = 1;
     };
     std::mutex mu;
@@ -828,9 +828,10 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
             HIP_TRY(hipMemsetAsync(nm.m, 0, (2 * L + 1) * sizeof(float), s));
             nm.v = nm.m + L;
             nm.vmax = nm.m + 2 * L;
-            if (o->amsgrad) {
+            if (o->amsgrad) {  // one tagged uint64 per tile; zero never matches a tick (>= 1)
                 const size_t nt = (L + stg::ADAM_TILE - 1) / stg::ADAM_TILE;
-                HIP_TRY(hipMalloc(&nm.tiles, 2 * nt * sizeof(uint32_t)));
+                HIP_TRY(hipMalloc(&nm.tiles, nt * sizeof(uint64_t)));
+                HIP_TRY(hipMemsetAsync(nm.tiles, 0, nt * sizeof(uint64_t), s));
             }
             nm.len = param_len;
             it = o->st.emplace(name, nm).first;
@@ -857,6 +858,7 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
     a.c2 = 1.0 - std::pow((double)o->b2, (double)tick);  // adam.cpp:43,68
     a.amsgrad = o->amsgrad;
     a.maximize = o->maximize;
+    a.tag = tick;
     if (grad_len) HIP_TRY(stg::launch_adam(a, s));
     return STG_OK;
 }

@@ -206,7 +206,8 @@ struct AdamLaunch {
     const uint32_t *d_grad_len; // device count (min'd with grad_len) or null
     float *m, *v;               // per-name moment arrays (param_len floats each)
     float *vmax;                // per-name running max (one float on the device)
-    uint32_t *tiles;            // amsgrad scratch: 2 words per ADAM_TILE tile
+    uint32_t *tiles;            // amsgrad look-back words: one uint64 per ADAM_TILE tile (zeroed at allocation)
+    uint32_t tag;               // amsgrad word tag: the name's tick of this call (>= 1)
     float b1, b2, eps, weight_decay;
     double lr, c1, c2;          // c = 1 - pow(b, tick), computed on the host (adam.cpp:42-43,67-68)
     bool amsgrad, maximize;
