@@ -119,3 +119,33 @@ def test_gather_slice_matches_oracle_without_gpu(oracle):
         for g in (1, 3, 8):
             for r in range(g):
                 assert gather_slice(n, r, g) == oracle.gather_slice(n, r, g)
+
+
+def test_new_entry_points_reject_bad_arguments_without_gpu():
+    """Argument checks of the §8f entry points run before any device call and
+    report through stg_last_error, as the reference's throws do."""
+    from stellatrain_amd._capi import lib
+    L = lib()
+    # wire: unknown flag bits; numel 0 is a no-op
+    assert L.stg_wire_encode_device(None, None, 4, 4, None, None, None) == -1
+    assert b"wire flag" in L.stg_last_error()
+    assert L.stg_wire_decode_device(None, None, 0, 3, None, None, None) == 0
+    # gather-add: more than 16 local GPUs, a rank outside the node
+    assert L.stg_gather_add_device(None, None, None, 17, 100, 0, None) == -4
+    a, b = C.c_uint64(), C.c_uint64()
+    assert L.stg_gather_slice(100, 3, 3, C.byref(a), C.byref(b)) == -1
+    # adam: amsgrad with more pairs than parameters (indices must be unique)
+    h = C.c_void_p()
+    assert L.stg_adam_create(0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, 0, C.byref(h)) == 0
+    assert L.stg_adam_optimize_raw_device(h, b"p", None, 10, None, None, 11, None, None) == -1
+    assert b"amsgrad" in L.stg_last_error()
+    assert L.stg_adam_get_state(h, b"never", None, None, 0, None, None, None) in (-1, -3)
+    assert L.stg_adam_destroy(h) == 0
+    # merge compress: null residual array
+    hc = C.c_void_p()
+    assert L.stg_codec_create(b"thresholdv16", 0, C.byref(hc)) in (0, -3)
+    if hc.value:
+        from stellatrain_amd.compressor import StgBucket
+        arr = (StgBucket * 1)()
+        assert L.stg_merge_compress_batch_device(hc, arr, None, 1, None) == -1
+        L.stg_codec_destroy(hc)
