@@ -239,3 +239,50 @@ def test_merge_compress_batch_error_feedback(gpu, oracle, method):
             expect[ii.view(np.uint32)] = 0.0
             assert np.array_equal(res[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), j
             assert np.array_equal(grads[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), j
+
+
+def test_merge_path_python_api(gpu, oracle):
+    """The whole node-side chain through the Python API, against the oracle
+    chain: gather-add (cpu_gather.cpp) -> compress + error feedback
+    (compress.cpp) -> wire encode/decode (comm_manager.cpp, u16 indices; a
+    bucket below 32768 elements so the shipped saturation never triggers) ->
+    MERGE decompress (cpu_optimize.cpp) -> sparse Adam (adam.cpp)."""
+    import torch
+    from stellatrain_amd import (CodecEngine, SparseAdam, gather_add, scatter_merge, wire_decode, wire_encode,
+                                 wire_flag)
+    n, g = 30000, 4
+    eng = CodecEngine()
+    eng.configure_compression("thresholdv16")
+    eng.configure_compression_ratio(0.99)
+    adam = SparseAdam(lr=1e-2)
+    ht, ha = oracle.tv16_new(), oracle.adam_new(lr=1e-2)
+    param = synth(n, seed_for(90, 9)) * np.float32(10)
+    pg = torch.from_numpy(param.copy()).to(gpu)
+    resid_o = np.zeros(n, np.float32)
+    resid_g = torch.zeros(n, dtype=torch.float32, device=gpu)
+    k = oracle.merge_numel(n, 0.99)
+    flag = wire_flag(n)
+    for it in range(3):
+        grads = [synth(n, seed_for(91 + r, it), D1) for r in range(g)]
+        dg = [torch.from_numpy(x.copy()).to(gpu) for x in grads]
+        for r in range(g):
+            oracle.gather_add(grads, resid_o, r)
+            gather_add(dg, resid_g, r)
+        co, io, vo = oracle.tv16_compress(ht, "p", grads[0], k)
+        io_full = np.zeros(k, np.uint32)
+        io_full[:co] = io[:co]
+        grads[0][io_full] = 0.0
+        resid_o = grads[0].copy()
+        idx, val, cnt = eng.compress_bucket("p", dg[0], world=1, residual=resid_g)
+        wi, wv = wire_encode(idx, val, flag)
+        ri, rv = wire_decode(wi, wv, flag)
+        oi, ov = oracle.wire_decode(*oracle.wire_encode(io_full, np.concatenate([vo[:co], np.zeros(k - co, np.float32)]),
+                                                        flag), flag)
+        mi, mv = oracle.merge_decompress(oi, ov, k, 1, n)
+        oracle.adam_apply(ha, "p", param, mv, mi)
+        gi, gv, gc = scatter_merge(ri, rv, k, 1, n)
+        adam.optimize_raw(pg, "p", gv, gi, grad_len=k, d_grad_len=gc)
+        assert np.array_equal(resid_g.cpu().numpy().view(np.uint32), resid_o.view(np.uint32))
+        assert np.array_equal(pg.cpu().numpy().view(np.uint32), param.view(np.uint32)), it
+    oracle.tv16_free(ht)
+    oracle.adam_free(ha)
