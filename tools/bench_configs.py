@@ -170,7 +170,7 @@ def host_inclusive(torch, method, mib, ratio, calls):
             "h2d_only_GBps": round(4.0 * n / h2d / 1e9, 2)}
 
 
-def c4_stream(torch, batches_timed):
+def c4_stream(torch, batches_timed, streams=1):
     from stellatrain_amd import ThresholdvCompressor16, merge_numel
     from stellatrain_amd._capi import lib
     from stellatrain_amd.shard import ShardPlan, c4_sizes
@@ -198,9 +198,20 @@ def c4_stream(torch, batches_timed):
     batches = [comp.bucket_array(rows[j:j + 16]) for j in range(0, len(rows), 16)]
     nrows = [len(rows[j:j + 16]) for j in range(0, len(rows), 16)]
 
+    # batch j on stream j % S (keys are distinct within a sweep, so batches are
+    # independent; a key's next batch is a sweep later, stream-ordered after
+    # the join); STG_TV16_INFLIGHT = S splits the workgroup slots between them
+    sts = [st] + [torch.cuda.Stream(dev) for _ in range(streams - 1)]
+
     def sweep():
-        for arr, nb in zip(batches, nrows):
-            comp.compress_batch_raw(arr, nb, st.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(st)
+        for x in sts[1:]:
+            x.wait_event(ev)
+        for j, (arr, nb) in enumerate(zip(batches, nrows)):
+            comp.compress_batch_raw(arr, nb, sts[j % streams].cuda_stream)
+        for x in sts[1:]:
+            st.wait_stream(x)
     sweep()  # first calls
     sweep()
     torch.cuda.synchronize()
@@ -212,6 +223,7 @@ def c4_stream(torch, batches_timed):
     comp.check_device()
     assert bool((counts.cpu().numpy() == np.array(ks)).all())
     return {"config": "C4 thresholdv16 k=1% stream of 1024 buckets 256 KiB-64 MiB (1 GPU)", "buckets": len(ids),
+            "streams": streams, "inflight": os.environ.get("STG_TV16_INFLIGHT", "1"),
             "bytes": 4 * total, "ms_per_sweep": round(el * 1e3, 3), "GBps_dense_in": round(4.0 * total / el / 1e9, 1),
             "launches": len(batches)}
 
@@ -396,6 +408,7 @@ def gather(torch, calls):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
+    p.add_argument("--c4-streams", type=int, default=1)
     p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply,ef,gather")
     a = p.parse_args()
     import torch
@@ -410,7 +423,7 @@ def main():
     if "e2e" in only:
         emit(host_inclusive(torch, "thresholdv16", 64, 0.99, 24))
     if "c4" in only:
-        emit(c4_stream(torch, 3))
+        emit(c4_stream(torch, 3, a.c4_streams))
     if "c5" in only:
         for kind in ("sgd", "adam", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))
