@@ -101,7 +101,7 @@ def main():
     if args.streams > 1:
         # S concurrent persistent launches sharing the device's two workgroup
         # slots per CU: one launch's exchange tail overlaps the others' streaming
-        os.environ.setdefault("STG_TV16_INFLIGHT", str(min(args.streams, 4)))
+        os.environ.setdefault("STG_TV16_INFLIGHT", str(min(args.streams, 2)))
     import torch
     import torch.distributed as dist
 
