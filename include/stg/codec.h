@@ -213,6 +213,21 @@ int stg_wire_encode_device(const uint32_t *d_idx, const float *d_val, size_t num
 int stg_wire_decode_device(const void *d_idx_in, const void *d_val_in, size_t numel, int flag, uint32_t *d_idx,
                            float *d_val, void *stream);
 
+/* One wire stream of a batched encode: the arguments of one encode call. */
+typedef struct stg_wire_stream {
+    const uint32_t *d_idx;
+    const float *d_val;
+    size_t numel;
+    int flag;
+    void *d_idx_out;
+    void *d_val_out;
+} stg_wire_stream_t;
+
+/* Batched stg_wire_encode_device: the same bytes as encoding streams[0..n-1]
+ * one by one (the tx queue of one iteration, comm_manager.cpp:573-640), in
+ * launches of up to 16 streams instead of one launch per stream. */
+int stg_wire_encode_batch_device(const stg_wire_stream_t *streams, size_t nstreams, void *stream);
+
 /* Synthetic fp32 buckets from the integer-only generator of SURVEY 8(d)
  * (dist 0 = D1, 1 = D2 heavy tail, 2 = D3 zeros with prob param/1e4);
  * bit-identical to oracle/stg_oracle.cpp:orc_synth_fill. */

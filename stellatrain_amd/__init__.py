@@ -9,6 +9,7 @@ from ._capi import CodecError, lib  # noqa: F401
 from .compressor import (Compressor, ThresholdvCompressor, ThresholdvCompressor16, TopkCompressor,  # noqa: F401
                          make_compressor)
 from .engine import (CodecEngine, SparseAdam, SparseSGD, api_numel, merge_numel, owner_of,  # noqa: F401
-                     gather_add, gather_slice, scatter_merge, wire_decode, wire_encode, wire_flag)
+                     gather_add, gather_slice, scatter_merge, wire_decode, wire_encode, wire_encode_batch,
+                     wire_flag)
 
 __version__ = "0.1.0"

@@ -76,6 +76,7 @@ _SIGS = {
                                          C.c_void_p]),
     "stg_wire_decode_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,
                                          C.c_void_p]),
+    "stg_wire_encode_batch_device": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p]),
     "stg_synth_fill_device": (C.c_int, [C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_uint32, C.c_void_p]),
     "stg_last_error": (C.c_char_p, []),
 }

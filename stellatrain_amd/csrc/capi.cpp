@@ -934,6 +934,45 @@ int stg_wire_encode_device(const uint32_t *d_idx, const float *d_val, size_t num
     return STG_OK;
 }
 
+int stg_wire_encode_batch_device(const stg_wire_stream_t *streams, size_t nstreams, void *stream) {
+    if (nstreams && !streams) return fail(STG_ERR_INVALID, "null stream array");
+    for (size_t i = 0; i < nstreams; ++i) {
+        const stg_wire_stream_t &w = streams[i];
+        if (w.flag & ~(STG_WIRE_U16_IDX | STG_WIRE_F16_VAL)) return fail(STG_ERR_INVALID, "unknown wire flag bits");
+        if (w.numel && (!w.d_idx || !w.d_val || !w.d_idx_out || !w.d_val_out))
+            return fail(STG_ERR_INVALID, "null argument");
+        if (w.numel > (size_t)STG_WG * 0xffffffull) return fail(STG_ERR_UNSUPPORTED, "wire stream too long for a batch");
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    stg::WireBatch b{};
+    uint64_t blocks = 0;
+    auto flush = [&]() -> int {
+        if (b.nb) HIP_TRY(stg::launch_wire_encode_batch(b, (uint32_t)blocks, s));
+        b = stg::WireBatch{};
+        blocks = 0;
+        return STG_OK;
+    };
+    for (size_t i = 0; i < nstreams; ++i) {
+        const stg_wire_stream_t &w = streams[i];
+        if (!w.numel) continue;
+        const uint64_t nbk = (w.numel + STG_WG - 1) / STG_WG;
+        if (b.nb == stg::WIRE_BATCH || blocks + nbk > 0x7fffffffull) {
+            int rc = flush();
+            if (rc) return rc;
+        }
+        stg::WireBucket &d = b.b[b.nb++];
+        d.idx = w.d_idx;
+        d.val = w.d_val;
+        d.idx_out = w.d_idx_out;
+        d.val_out = w.d_val_out;
+        d.n = w.numel;
+        d.flag = (uint32_t)w.flag;
+        d.blk0 = (uint32_t)blocks;
+        blocks += nbk;
+    }
+    return flush();
+}
+
 int stg_wire_decode_device(const void *d_idx_in, const void *d_val_in, size_t numel, int flag, uint32_t *d_idx,
                            float *d_val, void *stream) {
     if (flag & ~(STG_WIRE_U16_IDX | STG_WIRE_F16_VAL)) return fail(STG_ERR_INVALID, "unknown wire flag bits");

@@ -66,25 +66,42 @@ __device__ __forceinline__ uint32_t f32_to_u16_trunc(float f) {
     return (uint32_t)t & 0xffffu;
 }
 
+// one element of the encode (shared by the single and the batched launch)
+__device__ __forceinline__ void encode_one(const uint32_t *__restrict__ idx, const float *__restrict__ val, size_t i,
+                                           size_t simd_end, uint32_t flag, void *__restrict__ idx_out,
+                                           void *__restrict__ val_out) {
+    const uint32_t x = idx[i];
+    if (flag & 1u) {
+        const int32_t v = (int32_t)x;
+        const uint32_t w = i < simd_end ? (uint32_t)(uint16_t)(int16_t)min(max(v, -32768), 32767) : (x & 0xffffu);
+        static_cast<uint16_t *>(idx_out)[i] = (uint16_t)w;
+    } else {
+        static_cast<uint32_t *>(idx_out)[i] = x;
+    }
+    const float f = val[i];
+    if (flag & 2u)
+        static_cast<uint16_t *>(val_out)[i] =
+            (uint16_t)(i < simd_end ? f32_to_f16_rne(__float_as_uint(f)) : f32_to_u16_trunc(f));
+    else
+        static_cast<float *>(val_out)[i] = f;
+}
+
+// Batched encode: the launch's workgroups are dealt to the buckets by the
+// host-computed first-workgroup offsets (blk0), one element per lane.
+__global__ void __launch_bounds__(STG_WG) wire_encode_batch(WireBatch w) {
+    uint32_t b = 0;
+    while (b + 1 < w.nb && blockIdx.x >= w.b[b + 1].blk0) ++b;
+    const WireBucket &d = w.b[b];
+    const size_t i = (size_t)(blockIdx.x - d.blk0) * STG_WG + threadIdx.x;
+    if (i < d.n) encode_one(d.idx, d.val, i, d.n ? 8 * ((d.n - 1) / 8) : 0, d.flag, d.idx_out, d.val_out);
+}
+
 __global__ void __launch_bounds__(STG_WG) wire_encode(const uint32_t *__restrict__ idx, const float *__restrict__ val,
                                                       size_t n, size_t simd_end, uint32_t flag,
                                                       void *__restrict__ idx_out, void *__restrict__ val_out) {
     const size_t stride = (size_t)gridDim.x * STG_WG;
     for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < n; i += stride) {
-        const uint32_t x = idx[i];
-        if (flag & 1u) {
-            const int32_t v = (int32_t)x;
-            const uint32_t w = i < simd_end ? (uint32_t)(uint16_t)(int16_t)min(max(v, -32768), 32767) : (x & 0xffffu);
-            static_cast<uint16_t *>(idx_out)[i] = (uint16_t)w;
-        } else {
-            static_cast<uint32_t *>(idx_out)[i] = x;
-        }
-        const float f = val[i];
-        if (flag & 2u)
-            static_cast<uint16_t *>(val_out)[i] =
-                (uint16_t)(i < simd_end ? f32_to_f16_rne(__float_as_uint(f)) : f32_to_u16_trunc(f));
-        else
-            static_cast<float *>(val_out)[i] = f;
+        encode_one(idx, val, i, simd_end, flag, idx_out, val_out);
     }
 }
 
@@ -125,6 +142,12 @@ hipError_t launch_wire_encode(const uint32_t *idx, const float *val, size_t n, u
 hipError_t launch_wire_decode(const void *idx_in, const void *val_in, size_t n, uint32_t flag, uint32_t *idx,
                               float *val, int num_cu, hipStream_t s) {
     wire_decode<<<wire_blocks(n, num_cu), STG_WG, 0, s>>>(idx_in, val_in, n, simd_end(n), flag, idx, val);
+    return hipGetLastError();
+}
+
+hipError_t launch_wire_encode_batch(const WireBatch &w, uint32_t blocks, hipStream_t s) {
+    if (!w.nb || !blocks) return hipSuccess;
+    wire_encode_batch<<<blocks, STG_WG, 0, s>>>(w);
     return hipGetLastError();
 }
 

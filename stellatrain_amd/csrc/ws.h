@@ -222,6 +222,19 @@ struct GatherArgs {
     uint32_t nsrc;                 // N, the node's GPU count
 };
 hipError_t launch_gather_add(const GatherArgs &a, size_t start, size_t end, int num_cu, hipStream_t s);
+constexpr uint32_t WIRE_BATCH = 16;  // buckets per batched wire launch
+struct WireBucket {
+    const uint32_t *idx;
+    const float *val;
+    void *idx_out, *val_out;
+    uint64_t n;
+    uint32_t flag, blk0;  // blk0: first workgroup of this bucket in the launch
+};
+struct WireBatch {
+    WireBucket b[WIRE_BATCH];
+    uint32_t nb;
+};
+hipError_t launch_wire_encode_batch(const WireBatch &w, uint32_t blocks, hipStream_t s);
 hipError_t launch_wire_encode(const uint32_t *idx, const float *val, size_t n, uint32_t flag, void *idx_out,
                               void *val_out, int num_cu, hipStream_t s);
 hipError_t launch_wire_decode(const void *idx_in, const void *val_in, size_t n, uint32_t flag, uint32_t *idx,

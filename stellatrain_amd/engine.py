@@ -204,6 +204,26 @@ def wire_encode(idx, val, flag: int, idx_out=None, val_out=None):
     return idx_out, val_out
 
 
+class StgWireStream(C.Structure):
+    _fields_ = [("d_idx", C.c_void_p), ("d_val", C.c_void_p), ("numel", C.c_size_t), ("flag", C.c_int),
+                ("d_idx_out", C.c_void_p), ("d_val_out", C.c_void_p)]
+
+
+def wire_encode_batch(items):
+    """Batched wire encode (``stg_wire_encode_batch_device``): items of
+    (idx, val, flag, idx_out, val_out) device tensors; the same bytes as
+    ``wire_encode`` on each, in launches of up to 16 streams."""
+    import torch
+    if not items:
+        return
+    arr = (StgWireStream * len(items))()
+    for j, (idx, val, flag, io, vo) in enumerate(items):
+        arr[j] = StgWireStream(idx.data_ptr(), val.data_ptr(), idx.numel(), int(flag), io.data_ptr(), vo.data_ptr())
+    dev = items[0][0].device
+    check(lib().stg_wire_encode_batch_device(arr, len(items),
+                                             C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+
+
 def wire_decode(widx, wval, flag: int, idx=None, val=None):
     """Unpack a received stream (comm_manager.cpp:877-906) into int32 indices
     and float32 values on the device."""

@@ -72,3 +72,27 @@ def test_wire_codec_round_trip(gpu, oracle):
         assert np.array_equal(_u(ri.cpu().numpy()), di) and np.array_equal(_u(rv.cpu().numpy()), _u(dv))
         low = hi < 32768
         assert np.array_equal(di[low], hi[low])
+
+
+def test_wire_encode_batch_matches_single(gpu, oracle):
+    """stg_wire_encode_batch_device: 37 streams (three launches of <= 16),
+    mixed flags and lengths incl. 0 and < 8, byte-identical to the oracle."""
+    import torch
+    from stellatrain_amd import wire_encode_batch
+    rng = np.random.default_rng(7)
+    lens = [0, 1, 7, 9, 655, 4099, 65535] + [int(x) for x in rng.integers(1, 20000, 30)]
+    items, expect = [], []
+    for j, n in enumerate(lens):
+        flag = j % 4
+        idx, val = _stream(n, 500 + j, 65536 if flag & 1 else 1 << 30)
+        di = torch.from_numpy(idx.view(np.int32)).to(gpu)
+        dv = torch.from_numpy(val).to(gpu)
+        io = torch.full((max(n, 1),), -1, dtype=torch.int16 if flag & 1 else torch.int32, device=gpu)[:n]
+        vo = torch.full((max(n, 1),), -1, dtype=torch.int16 if flag & 2 else torch.float32, device=gpu)[:n]
+        items.append((di, dv, flag, io, vo))
+        expect.append(oracle.wire_encode(idx, val, flag))
+    wire_encode_batch(items)
+    torch.cuda.synchronize()
+    for (di, dv, flag, io, vo), (oi, ov) in zip(items, expect):
+        assert np.array_equal(_u(io.cpu().numpy()), _u(oi))
+        assert np.array_equal(_u(vo.cpu().numpy()), _u(ov))

@@ -324,6 +324,21 @@ def apply_and_wire(torch, calls):
         out.append({"config": f"WIRE flag={flag} k={k}", "encode_us": round(us_e, 2), "decode_us": round(us_d, 2),
                     "encode_alg_GBps": round((8.0 * k + wb) / us_e / 1e3, 1),
                     "decode_alg_GBps": round((8.0 * k + wb) / us_d / 1e3, 1)})
+    # the C4 stream's 1024 (idx, val) streams: one launch each vs batched
+    from stellatrain_amd import wire_encode_batch
+    from stellatrain_amd.shard import c4_sizes
+    ks4 = [merge_numel(x, 0.99) for x in c4_sizes()]
+    flat_i = torch.zeros(sum(ks4), dtype=torch.int32, device=dev)
+    flat_v = torch.zeros(sum(ks4), dtype=torch.float32, device=dev)
+    out_i = torch.empty(sum(ks4), dtype=torch.int16, device=dev)
+    out_v = torch.empty(sum(ks4), dtype=torch.float32, device=dev)
+    o4 = np.concatenate([[0], np.cumsum(ks4)]).astype(np.int64)
+    items = [(flat_i[o4[j]:o4[j + 1]], flat_v[o4[j]:o4[j + 1]], 1, out_i[o4[j]:o4[j + 1]], out_v[o4[j]:o4[j + 1]])
+             for j in range(len(ks4))]
+    us_one = _time_loop(torch, st, lambda s: [wire_encode(a, b, f, c, d) for a, b, f, c, d in items], 4, 1)
+    us_bat = _time_loop(torch, st, lambda s: wire_encode_batch(items), 4, 1)
+    out.append({"config": f"WIRE encode of the C4 stream's {len(ks4)} streams (u16 idx)",
+                "one_launch_per_stream_us": round(us_one, 1), "batched_us": round(us_bat, 1)})
     return out
 
 
