@@ -869,7 +869,6 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
 int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *host_v, uint32_t len,
                        float *host_vmax, uint32_t *tick_out, void *stream) {
     if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(o->device));
     stg_adam::Name nm;
     {
         std::lock_guard<std::mutex> g(o->mu);
@@ -877,6 +876,7 @@ int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *hos
         if (it == o->st.end()) return fail(STG_ERR_INVALID, "no Adam state for this name");
         nm = it->second;
     }
+    HIP_TRY(hipSetDevice(o->device));
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     const size_t c = std::min(len, nm.len);
     if (host_m) HIP_TRY(hipMemcpy(host_m, nm.m, c * sizeof(float), hipMemcpyDeviceToHost));
