@@ -268,13 +268,16 @@ def c5_round_trip(torch, steps, kind="sgd"):
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
+    t0 = time.perf_counter()
     for s in range(steps):
         step(s)
+    host_us = (time.perf_counter() - t0) * 1e6 / steps  # enqueue cost of the three Python calls
     e1.record(st)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / steps
     alg = 4.0 * n + 8.0 * k + (16.0 if kind == "sgd" else 24.0) * k
     return {"config": f"C5 thresholdv16 compress + decompress + {label} 64 MiB k={k}", "us_per_step": round(us, 2),
+            "host_enqueue_us_per_step": round(host_us, 2),
             "GBps_dense_in": round(4.0 * n / us / 1e3, 1), "alg_GBps": round(alg / us / 1e3, 1)}
 
 
