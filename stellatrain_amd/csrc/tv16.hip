@@ -50,6 +50,9 @@ namespace stg {
 namespace {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+#ifndef STG_EF_AUX
+#define STG_EF_AUX 2  // cache policy of the fused residual stores (2: nontemporal)
+#endif
 
 constexpr uint32_t FWG = 1024;      // workgroup: 16 waves
 constexpr uint32_t FNW = FWG / 64;
@@ -435,7 +438,7 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
         asm volatile("" : "+v"(voff));
         u4v t4;
         t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
-        __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NS * 1024u), 0, 2 /* nt */);
+        __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NS * 1024u), 0, STG_EF_AUX /* 2 = nt */);
     };
     auto load = [&](uint32_t m) -> float4 {
         uint32_t voff = lane_line * 64u + q * 16u;
