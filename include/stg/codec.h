@@ -139,10 +139,14 @@ int stg_codec_check(stg_codec_t h);
 /* MERGE decompress (cpu_optimize.cpp:40-72): `world` rank streams of
  * `per_rank` (idx, val) pairs each, laid out back to back, are scattered
  * into a dense zeroed scratch of n floats in rank order (index_put_, no
- * accumulate, per rank), summed, divided by `world`, and gathered at the
- * union of indices.  Output is index-ascending; *d_out_count (device) gets
- * the union size.  d_dense (n floats) and d_mark (n bytes) are caller
- * scratch. */
+ * accumulate, per rank: of a rank's duplicated indices -- e.g. the wire
+ * format's u16 saturation -- the last occurrence wins), summed, divided by
+ * `world`, and gathered at the union of indices (one entry per index,
+ * unique1d :14-24).  world > 1: output index-ascending, d_dense (n floats,
+ * zero) and d_mark (n bytes, zero, 16-byte aligned) are caller scratch and
+ * are left zero.  world == 1: no dense scratch; the winners in stream order.
+ * Indices >= n are dropped.  *d_out_count (device) gets the union size.
+ * Internal scratch is kept per (device, stream). */
 int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t per_rank, int world, size_t n,
                              float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
                              uint32_t *d_out_count, void *stream);
@@ -183,6 +187,10 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
                                  const uint32_t *d_grad_len, void *stream);
 int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *host_v, uint32_t len,
                        float *host_vmax, uint32_t *tick_out, void *stream);
+/* Synchronises `stream` and reports the handle's sticky device failure word:
+ * STG_ERR_DEVICE if an amsgrad look-back ever timed out (its updates used an
+ * incomplete running max), STG_OK otherwise. */
+int stg_adam_check(stg_adam_t o, void *stream);
 
 /* Intra-node gather-add before the codec (ModuleCpuGather::run,
  * engine/modules/cpu_gather.cpp:59-87, add_arrays misc/array_util.h:12-54).

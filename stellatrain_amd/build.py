@@ -13,6 +13,17 @@ def build_codec(jobs: int = 8) -> str:
     return os.path.join(HERE, "libstg_codec.so")
 
 
+def build_shim() -> str:
+    """tests/cpp/shim_factory: the reference engine's codec factory and MERGE
+    call site compiled against include/stg/compressor.h (test binary, run by
+    tests/test_gpu_api.py on the GPU box)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "shim_factory")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "shim_factory.cpp"), "-o", exe, "-L", HERE, "-lstg_codec",
+                    "-Wl,-rpath,$ORIGIN/../../stellatrain_amd"], check=True)
+    return exe
+
+
 def build_oracle(ref: bool | None = None) -> None:
     import sys
     sys.path.insert(0, ROOT)
@@ -23,3 +34,4 @@ def build_oracle(ref: bool | None = None) -> None:
 if __name__ == "__main__":
     print(build_codec())
     build_oracle()
+    print(build_shim())

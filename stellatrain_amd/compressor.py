@@ -73,7 +73,9 @@ class Compressor:
         """``Compressor::compress`` (compressor.h:30); returns the pair count."""
         if _is_torch(src) and src.is_cuda:
             cnt = self.compress_async(name, src, k, dst_idx, dst_val, idx_offset)
-            return int(cnt.item())
+            c = int(cnt.item())
+            self.check_device()  # the synchronous form surfaces device-side failures as errors
+            return c
         return self._compress_host(name, src, k, dst_idx, dst_val, idx_offset)
 
     def compress_async(self, name: str, src, k: int, dst_idx, dst_val, idx_offset: int = 0, count=None):

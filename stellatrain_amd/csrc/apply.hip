@@ -11,6 +11,15 @@
 // unordered_set order is unspecified and SGD is per-index).  world == 1 needs
 // no dense scratch: out = (0.0f + v) / 1.0f in stream order.
 //
+// Duplicate indices within a rank (the wire format's signed u16 saturation
+// maps every index >= 32768 of an 8-wide block to 32767, comm_manager.cpp:
+// 509-529): index_put_ without accumulate keeps the LAST occurrence (the
+// reference's per-rank CPU index_put_ runs sequentially at these sizes), and
+// unique1d (:14-24) leaves one entry per index.  Every rank therefore first
+// elects its winner per index (atomicMax of position + 1 into a u32 scratch
+// that is zero between calls), and only the winner scatters (and re-zeroes the
+// scratch word); world == 1 keeps the winners in stream order.
+//
 // Sparse SGD: optim/sgd.cpp:34-55 and the scalar loop :221-263 with the FMA
 // shapes GCC -O3 -march=broadwell emits (read from the object code):
 //   wd:        g = fmaf(wd, x, g)                        (vfmadd231ss, :235)
@@ -38,24 +47,38 @@ namespace stg {
 
 namespace {
 
-constexpr uint32_t MARK_TILE = STG_WG * 16;  // marks per tile (one uint4 per lane)
+constexpr uint32_t MARK_TILE = MERGE_TILE;  // marks (or pairs) per tile (one uint4 of marks per lane)
 
-__global__ void __launch_bounds__(STG_WG) merge_world1(const uint32_t *__restrict__ idx, const float *__restrict__ val,
-                                                       size_t m, uint32_t *__restrict__ out_idx,
-                                                       float *__restrict__ out_val, uint32_t *out_count) {
-    const size_t stride = (size_t)gridDim.x * STG_WG;
-    for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
-        out_idx[i] = idx[i];
-        out_val[i] = (0.0f + val[i]) / 1.0f;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = (uint32_t)m;
-}
-
-__global__ void __launch_bounds__(STG_WG) scatter_rank(const uint32_t *__restrict__ idx, const float *__restrict__ val,
-                                                       size_t m, float *__restrict__ dense, uint8_t *__restrict__ mark) {
+// Winner election: win[j] = 1 + the last position of index j in the rank's
+// stream (indices >= n are dropped: the reference would throw on them).
+__global__ void __launch_bounds__(STG_WG) win_mark(const uint32_t *__restrict__ idx, size_t m, size_t n,
+                                                   uint32_t *__restrict__ win) {
     const size_t stride = (size_t)gridDim.x * STG_WG;
     for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
         const uint32_t j = idx[i];
+        if (j < n) atomicMax(&win[j], (uint32_t)i + 1u);
+    }
+}
+
+// world == 1, pass 1: winners per tile of MARK_TILE pairs.
+__global__ void __launch_bounds__(STG_WG) win_count(const uint32_t *__restrict__ idx, size_t m, size_t n,
+                                                    const uint32_t *__restrict__ win, uint32_t *__restrict__ tile_cnt);
+// world == 1, pass 2: ordered compaction of the winners (look-up of the
+// earlier tiles' counts), re-zeroing their scratch words.
+__global__ void __launch_bounds__(STG_WG) win_emit1(const uint32_t *__restrict__ idx, const float *__restrict__ val,
+                                                    size_t m, size_t n, uint32_t ntiles, uint32_t *__restrict__ win,
+                                                    const uint32_t *__restrict__ tile_cnt,
+                                                    uint32_t *__restrict__ out_idx, float *__restrict__ out_val,
+                                                    uint32_t *out_count);
+
+__global__ void __launch_bounds__(STG_WG) scatter_rank(const uint32_t *__restrict__ idx, const float *__restrict__ val,
+                                                       size_t m, size_t n, uint32_t *__restrict__ win,
+                                                       float *__restrict__ dense, uint8_t *__restrict__ mark) {
+    const size_t stride = (size_t)gridDim.x * STG_WG;
+    for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
+        const uint32_t j = idx[i];
+        if (j >= n || win[j] != (uint32_t)i + 1u) continue;  // a later occurrence wins
+        win[j] = 0;
         dense[j] += val[i];
         mark[j] = 1;
     }
@@ -125,6 +148,73 @@ __global__ void __launch_bounds__(STG_WG) mark_emit(uint8_t *__restrict__ mark, 
                 out_val[P + r] = dense[j] / world;
                 dense[j] = 0.f;  // leave the scratch zeroed for the next call
                 mark[j] = 0;
+                ++r;
+            }
+        }
+        P += tc;
+    }
+    if (w == 0 && tid == 0) *out_count = (uint32_t)total;
+}
+
+__global__ void __launch_bounds__(STG_WG) win_count(const uint32_t *__restrict__ idx, size_t m, size_t n,
+                                                    const uint32_t *__restrict__ win, uint32_t *__restrict__ tile_cnt) {
+    __shared__ uint32_t s[STG_WAVES];
+    const size_t e0 = (size_t)blockIdx.x * MARK_TILE;
+    uint32_t c = 0;
+    for (uint32_t b = threadIdx.x; b < MARK_TILE; b += STG_WG) {
+        const size_t i = e0 + b;
+        if (i < m) {
+            const uint32_t j = idx[i];
+            c += j < n && win[j] == (uint32_t)i + 1u;
+        }
+    }
+    c = wave_sum(c);
+    if (__lane_id() == 0) s[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) t += s[w];
+        tile_cnt[blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(STG_WG) win_emit1(const uint32_t *__restrict__ idx, const float *__restrict__ val,
+                                                    size_t m, size_t n, uint32_t ntiles, uint32_t *__restrict__ win,
+                                                    const uint32_t *__restrict__ tile_cnt,
+                                                    uint32_t *__restrict__ out_idx, float *__restrict__ out_val,
+                                                    uint32_t *out_count) {
+    __shared__ uint64_t sh64[STG_WAVES];
+    __shared__ uint32_t sh[STG_WAVES + 1];
+    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+    const uint32_t t_begin = (uint32_t)((uint64_t)w * ntiles / G);
+    const uint32_t t_end = (uint32_t)((uint64_t)(w + 1) * ntiles / G);
+    uint64_t tot = 0, bef = 0;
+    for (uint32_t i = tid; i < ntiles; i += STG_WG) {
+        const uint32_t c = tile_cnt[i];
+        tot += c;
+        if (i < t_begin) bef += c;
+    }
+    const uint64_t total = wg_sum64(tot, sh64);
+    uint64_t P = wg_sum64(bef, sh64);
+    constexpr uint32_t PER = MARK_TILE / STG_WG;  // 16 consecutive pairs per lane
+    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+        const size_t e = (size_t)tile * MARK_TILE + (size_t)PER * tid;
+        uint32_t keep = 0;  // bit b: pair e + b wins
+        for (uint32_t b = 0; b < PER; ++b) {
+            const size_t i = e + b;
+            if (i < m) {
+                const uint32_t j = idx[i];
+                if (j < n && win[j] == (uint32_t)i + 1u) keep |= 1u << b;
+            }
+        }
+        uint32_t tc;
+        uint32_t r = wg_excl_scan((uint32_t)__popc(keep), sh, &tc);
+        for (uint32_t b = 0; b < PER; ++b) {
+            if (keep >> b & 1u) {
+                const uint32_t j = idx[e + b];
+                out_idx[P + r] = j;
+                out_val[P + r] = (0.0f + val[e + b]) / 1.0f;
+                win[j] = 0;  // scratch back to zero for the next call
                 ++r;
             }
         }
@@ -295,7 +385,11 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
             const uint32_t p = p0 + threadIdx.x;
             if (p < tile) {
                 uint64_t w = ld_sc1(&words[p]);
-                for (uint32_t spins = 0; (uint32_t)(w >> 32) != tag && spins < (1u << 22); ++spins) {
+                for (uint32_t spins = 0; (uint32_t)(w >> 32) != tag; ++spins) {
+                    if (spins >= (1u << 22)) {  // starved predecessor: flag it (stg_adam_check), never use a stale word silently
+                        g_or(a.fail, FAIL_SPIN_TIMEOUT);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                     w = ld_sc1(&words[p]);
                 }
@@ -356,16 +450,25 @@ hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, siz
 
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,
-                                uint32_t *out_count, uint32_t *scratch_tiles, int num_cu, hipStream_t s) {
+                                uint32_t *out_count, uint32_t *scratch_tiles, uint32_t *win, int num_cu,
+                                hipStream_t s) {
     const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((per_rank + STG_WG - 1) / STG_WG,
                                                                           (size_t)num_cu * 8));
     if (world == 1) {
-        merge_world1<<<blocks, STG_WG, 0, s>>>(idx, val, per_rank, out_idx, out_val, out_count);
+        if (!per_rank) return hipMemsetAsync(out_count, 0, sizeof(uint32_t), s);
+        win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win);
+        const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
+        win_count<<<nt, STG_WG, 0, s>>>(idx, per_rank, n, win, scratch_tiles);
+        const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)num_cu, nt));
+        win_emit1<<<G, STG_WG, 0, s>>>(idx, val, per_rank, n, nt, win, scratch_tiles, out_idx, out_val, out_count);
         return hipGetLastError();
     }
-    for (int r = 0; r < world; ++r)
-        scatter_rank<<<blocks, STG_WG, 0, s>>>(idx + (size_t)r * per_rank, val + (size_t)r * per_rank, per_rank,
-                                               dense, mark);
+    for (int r = 0; r < world; ++r) {
+        if (!per_rank) break;
+        const uint32_t *ir = idx + (size_t)r * per_rank;
+        win_mark<<<blocks, STG_WG, 0, s>>>(ir, per_rank, n, win);
+        scatter_rank<<<blocks, STG_WG, 0, s>>>(ir, val + (size_t)r * per_rank, per_rank, n, win, dense, mark);
+    }
     const uint32_t ntiles = (uint32_t)((n + MARK_TILE - 1) / MARK_TILE);
     mark_count<<<std::max<uint32_t>(1, ntiles), STG_WG, 0, s>>>(mark, n, scratch_tiles);
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)num_cu, ntiles));

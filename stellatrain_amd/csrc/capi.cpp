@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <array>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -237,6 +238,7 @@ struct stg_sgd {
 
 struct stg_adam {
     int device = 0;
+    uint32_t *fail = nullptr;  // device failure word (amsgrad look-back timeout)
     float lr, b1, b2, eps, weight_decay;
     bool amsgrad, maximize;
     struct Name {
@@ -248,6 +250,7 @@ struct stg_adam {
     std::unordered_map<std::string, Name> st;
     ~stg_adam() {
         (void)hipSetDevice(device);
+        (void)hipFree(fail);
         for (auto &kv : st) {
             (void)hipFree(kv.second.m);
             (void)hipFree(kv.second.tiles);
@@ -473,6 +476,49 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
     return STG_OK;
 }
 
+// MERGE decompress scratch, one per (device, stream): the per-tile counts and
+// the u32 winner words (zero between calls).  Keyed like the codec
+// workspaces, so merges issued from one thread on several streams or devices
+// never share scratch.  Growing waits for the stream's in-flight work.
+struct MergeScratch {
+    std::mutex mu;
+    int device = 0;
+    uint32_t *tiles = nullptr, *win = nullptr;
+    size_t cap_tiles = 0, cap_win = 0;
+};
+std::mutex g_merge_mu;
+std::map<std::pair<int, hipStream_t>, std::unique_ptr<MergeScratch>> g_merge;
+
+MergeScratch *merge_scratch(int dev, hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_merge_mu);
+    auto &slot = g_merge[{dev, s}];
+    if (!slot) { slot = std::make_unique<MergeScratch>(); slot->device = dev; }
+    return slot.get();
+}
+
+// Caller holds m->mu.
+int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_rank) {
+    const size_t tiles = (std::max(n, per_rank) + stg::MERGE_TILE - 1) / stg::MERGE_TILE + 1;
+    if (tiles > m->cap_tiles) {
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(m->tiles);
+        m->tiles = nullptr;
+        HIP_TRY(hipMalloc(&m->tiles, tiles * sizeof(uint32_t)));
+        m->cap_tiles = tiles;
+    }
+    const size_t words = std::max<size_t>(n, 1);
+    if (words > m->cap_win) {
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(m->win);
+        m->win = nullptr;
+        const size_t c = std::max(words, m->cap_win + m->cap_win / 2);
+        HIP_TRY(hipMalloc(&m->win, c * sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(m->win, 0, c * sizeof(uint32_t), s));
+        m->cap_win = c;
+    }
+    return STG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -579,7 +625,7 @@ int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, si
         if ((rc = ws->grow(ws->h_val, co, std::max<size_t>(idx_cap, 1)))) return rc;
         ws->cap_out = co;
         if (!ws->h_count) HIP_TRY(hipMalloc(&ws->h_count, sizeof(uint32_t)));
-        if (!ws->pinned_count) HIP_TRY(hipHostMalloc(&ws->pinned_count, sizeof(uint32_t)));
+        if (!ws->pinned_count) HIP_TRY(hipHostMalloc(&ws->pinned_count, 2 * sizeof(uint32_t)));
         if (n) HIP_TRY(hipMemcpyAsync(ws->h_src, src, n * sizeof(float), hipMemcpyHostToDevice, s));
     }
     // threshold-v keys its state by the caller's (host) src pointer
@@ -591,7 +637,15 @@ int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, si
         HIP_TRY(hipMemcpyAsync(dst_idx, ws->h_idx, idx_cap * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(dst_val, ws->h_val, std::min(idx_cap, val_cap) * sizeof(float), hipMemcpyDeviceToHost, s));
     }
+    // the workspace's sticky failure word rides along: a device-side failure
+    // (a bounded wait that gave up) is an error, never a silent wrong result
+    HIP_TRY(hipMemcpyAsync(ws->pinned_count + 1, ws->d.fail, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (ws->pinned_count[1]) {
+        char b[96];
+        snprintf(b, sizeof b, "device failure flags 0x%x (details: stg_codec_check)", ws->pinned_count[1]);
+        return fail(STG_ERR_DEVICE, b);
+    }
     *out_count = *ws->pinned_count;
     return STG_OK;
 }
@@ -692,21 +746,19 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
     if (world < 1) return fail(STG_ERR_INVALID, "world must be >= 1");
     if (world > 1 && (!d_dense || !d_mark)) return fail(STG_ERR_INVALID, "dense/mark scratch required for world > 1");
     if (world > 1 && (reinterpret_cast<uintptr_t>(d_mark) & 15u)) return fail(STG_ERR_INVALID, "mark scratch must be 16-byte aligned");
+    if (n >= (size_t(1) << 32) || per_rank >= (size_t(1) << 32))
+        return fail(STG_ERR_UNSUPPORTED, "more than 2^32-1 elements (uint32 indices)");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     int ncu = 256;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    static thread_local uint32_t *tiles = nullptr;
-    static thread_local size_t tiles_cap = 0;
-    const size_t need = (n + STG_WG * 16 - 1) / (STG_WG * 16) + 1;
-    if (world > 1 && need > tiles_cap) {
-        HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-        (void)hipFree(tiles);
-        HIP_TRY(hipMalloc(&tiles, need * sizeof(uint32_t)));
-        tiles_cap = need;
-    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    MergeScratch *ms = merge_scratch(dev, s);
+    std::lock_guard<std::mutex> g(ms->mu);
+    int rc = merge_scratch_ensure(ms, s, n, per_rank);
+    if (rc) return rc;
     HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, n, d_dense, d_mark, d_out_idx, d_out_val,
-                                      d_out_count, tiles, ncu, static_cast<hipStream_t>(stream)));
+                                      d_out_count, ms->tiles, ms->win, ncu, s));
     return STG_OK;
 }
 
@@ -822,6 +874,10 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
     uint32_t tick;
     {
         std::lock_guard<std::mutex> g(o->mu);
+        if (!o->fail) {  // the handle's failure word, allocated with its first state
+            HIP_TRY(hipMalloc(&o->fail, sizeof(uint32_t)));
+            HIP_TRY(hipMemsetAsync(o->fail, 0, sizeof(uint32_t), s));
+        }
         auto it = o->st.find(name);
         if (it == o->st.end()) {  // adam.cpp:28-35: zeroed m and v, vmax 0, tick 1
             stg_adam::Name nm;
@@ -862,6 +918,7 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
     a.amsgrad = o->amsgrad;
     a.maximize = o->maximize;
     a.tag = tick;
+    a.fail = o->fail;
     if (grad_len) HIP_TRY(stg::launch_adam(a, s));
     return STG_OK;
 }
@@ -883,6 +940,16 @@ int stg_adam_get_state(stg_adam_t o, const char *name, float *host_m, float *hos
     if (host_v) HIP_TRY(hipMemcpy(host_v, nm.v, c * sizeof(float), hipMemcpyDeviceToHost));
     if (host_vmax) HIP_TRY(hipMemcpy(host_vmax, nm.vmax, sizeof(float), hipMemcpyDeviceToHost));
     if (tick_out) *tick_out = nm.tick;
+    return STG_OK;
+}
+
+int stg_adam_check(stg_adam_t o, void *stream) {
+    if (!o) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    uint32_t f = 0;
+    if (o->fail) HIP_TRY(hipMemcpy(&f, o->fail, sizeof f, hipMemcpyDeviceToHost));
+    if (f) return fail(STG_ERR_DEVICE, "adam: amsgrad look-back timed out (a predecessor tile never published)");
     return STG_OK;
 }
 

@@ -180,7 +180,9 @@ hipError_t launch_synth(float *dst, size_t n, uint64_t seed, int dist, uint32_t 
 
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,
-                                uint32_t *out_count, uint32_t *scratch_tiles, int num_cu, hipStream_t s);
+                                uint32_t *out_count, uint32_t *scratch_tiles, uint32_t *win, int num_cu,
+                                hipStream_t s);
+constexpr uint32_t MERGE_TILE = STG_WG * 16;  // pairs / marks per scatter-merge tile
 
 struct SgdLaunch {
     float *param;
@@ -208,6 +210,7 @@ struct AdamLaunch {
     float *vmax;                // per-name running max (one float on the device)
     uint32_t *tiles;            // amsgrad look-back words: one uint64 per ADAM_TILE tile (zeroed at allocation)
     uint32_t tag;               // amsgrad word tag: the name's tick of this call (>= 1)
+    uint32_t *fail;             // sticky device failure word of the optimizer handle
     float b1, b2, eps, weight_decay;
     double lr, c1, c2;          // c = 1 - pow(b, tick), computed on the host (adam.cpp:42-43,67-68)
     bool amsgrad, maximize;

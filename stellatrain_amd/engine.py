@@ -131,7 +131,9 @@ class CodecEngine:
 def scatter_merge(idx, val, per_rank: int, world: int, n: int, dense=None, mark=None, out_idx=None, out_val=None,
                   count=None):
     """MERGE decompress on the device (cpu_optimize.cpp:40-72).  ``dense``
-    (float32[n]) and ``mark`` (uint8[n]) must be zero and are left zero."""
+    (float32[n]) and ``mark`` (uint8[n]) must be zero and are left zero.  Per
+    rank, the last occurrence of a duplicated index wins (index_put_ without
+    accumulate); the output holds each index once (unique1d)."""
     import torch
     dev = idx.device
     if out_idx is None:
@@ -310,6 +312,11 @@ class SparseAdam:
             self._h, name.encode(), C.c_void_p(param.data_ptr()), param.numel(), C.c_void_p(grad.data_ptr()),
             C.c_void_p(gidx.data_ptr()), n, C.c_void_p(d_grad_len.data_ptr()) if d_grad_len is not None else None,
             C.c_void_p(torch.cuda.current_stream(param.device.index).cuda_stream)))
+
+    def check_device(self) -> None:
+        """Raise if a device-side failure was flagged (amsgrad look-back timeout)."""
+        import torch
+        check(lib().stg_adam_check(self._h, C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)))
 
     def state(self, name: str, n: int):
         """(m, v, vmax, tick) of a name, or None before its first call."""

@@ -286,3 +286,57 @@ def test_merge_path_python_api(gpu, oracle):
         assert np.array_equal(pg.cpu().numpy().view(np.uint32), param.view(np.uint32)), it
     oracle.tv16_free(ht)
     oracle.adam_free(ha)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_saturated_wire_merge_adam(gpu, oracle, world):
+    """a bucket with 32768 <= numel < 65536 travels with u16 indices
+    whose 8-wide blocks saturate every index >= 32768 to 32767
+    (comm_manager.cpp:509-529), so a decoded rank stream repeats 32767.  The
+    MERGE decompress keeps the last occurrence per rank (index_put_ without
+    accumulate) and one entry per index (unique1d), and the sparse Adam after
+    it sees unique indices: parity with the oracle chain, bit-exact."""
+    import torch
+    from stellatrain_amd import SparseAdam, ThresholdvCompressor16, scatter_merge, wire_decode, wire_encode, wire_flag
+    n = 50000
+    k = oracle.merge_numel(n, 0.99, world)
+    flag = wire_flag(n)
+    comp = ThresholdvCompressor16()
+    ht = oracle.tv16_new()
+    ha = oracle.adam_new(lr=1e-2)
+    adam = SparseAdam(lr=1e-2)
+    param = synth(n, seed_for(70, 1)) * np.float32(10)
+    pg = torch.from_numpy(param.copy()).to(gpu)
+    for it in range(2):
+        ri_all, rv_all, oi_all, ov_all = [], [], [], []
+        for r in range(world):
+            src = synth(n, seed_for(71 + r, it))
+            co, io, vo = oracle.tv16_compress(ht, f"r{r}", src, k)
+            idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+            val = torch.zeros(k, dtype=torch.float32, device=gpu)
+            assert comp.compress(f"r{r}", torch.from_numpy(src).to(gpu), k, idx, val) == co
+            wi, wv = wire_encode(idx, val, flag)
+            ri, rv = wire_decode(wi, wv, flag)
+            oi, ov = oracle.wire_decode(*oracle.wire_encode(io, vo, flag), flag)
+            assert np.array_equal(ri.cpu().numpy().view(np.uint32), oi)
+            ri_all.append(ri)
+            rv_all.append(rv)
+            oi_all.append(oi)
+            ov_all.append(ov)
+        ri, rv = torch.cat(ri_all), torch.cat(rv_all)
+        oi, ov = np.concatenate(oi_all), np.concatenate(ov_all)
+        assert np.count_nonzero(oi == 32767) > 1  # the saturation produced duplicates
+        mi, mv = oracle.merge_decompress(oi, ov, k, world, n)
+        dense = torch.zeros(n, dtype=torch.float32, device=gpu) if world > 1 else None
+        mark = torch.zeros(n, dtype=torch.uint8, device=gpu) if world > 1 else None
+        gi, gv, gc = scatter_merge(ri, rv, k, world, n, dense=dense, mark=mark)
+        m = int(gc.item())
+        assert m == mi.size
+        a_i, a_v = _sorted_pairs(gi[:m].cpu().numpy(), gv[:m].cpu().numpy())
+        assert np.array_equal(a_i, mi) and np.array_equal(a_v.view(np.uint32), mv.view(np.uint32))
+        oracle.adam_apply(ha, "p", param, mv, mi)
+        adam.optimize_raw(pg, "p", gv, gi, grad_len=k * world, d_grad_len=gc)
+        assert np.array_equal(pg.cpu().numpy().view(np.uint32), param.view(np.uint32)), it
+    adam.check_device()
+    oracle.tv16_free(ht)
+    oracle.adam_free(ha)
