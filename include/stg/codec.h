@@ -132,6 +132,10 @@ int stg_codec_get_state(stg_codec_t h, const char *key, const void *key_ptr, flo
 int stg_codec_set_timing(stg_codec_t h, int enable);
 int stg_codec_get_timing(stg_codec_t h, double *ms3, uint64_t *calls);
 
+/* Diagnostics: the first n (<= 64) scratch words of the handle's workspace
+ * for `stream` (phase stamps of builds with STG_FILL_STAMPS); syncs. */
+int stg_codec_debug_words(stg_codec_t h, void *stream, uint32_t *out, int n);
+
 /* Checks the device-side failure word of every workspace of this handle
  * (e.g. a regime-B candidate set larger than the build supports); syncs. */
 int stg_codec_check(stg_codec_t h);

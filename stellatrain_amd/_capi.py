@@ -49,6 +49,7 @@ _SIGS = {
     "stg_codec_get_state": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.POINTER(C.c_float),
                                       C.POINTER(C.c_float), C.c_void_p]),
     "stg_codec_check": (C.c_int, [C.c_void_p]),
+    "stg_codec_debug_words": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]),
     "stg_codec_set_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "stg_codec_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "stg_scatter_merge_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_size_t, C.c_void_p,

@@ -91,7 +91,7 @@ struct Workspace {
         const size_t o_cp = carve(sizeof(stg::CallParams));
         const size_t o_rs = carve(sizeof(stg::RSel));
         const size_t o_fail = carve(sizeof(uint32_t));
-        const size_t o_cand = carve(sizeof(uint64_t) * stg::SORT_CAP);
+        const size_t o_cand = carve(sizeof(uint32_t) * stg::CAND_WORDS * stg::MAX_BATCH);
         const size_t o_misc = carve(sizeof(uint32_t) * 64);
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
@@ -103,7 +103,7 @@ struct Workspace {
         d.cp = reinterpret_cast<stg::CallParams *>(b + o_cp);
         d.rsel = reinterpret_cast<stg::RSel *>(b + o_rs);
         d.fail = reinterpret_cast<uint32_t *>(b + o_fail);
-        d.cand = reinterpret_cast<uint64_t *>(b + o_cand);
+        d.cand = reinterpret_cast<uint32_t *>(b + o_cand);
         d.misc = reinterpret_cast<uint32_t *>(b + o_misc);
         return STG_OK;
     }
@@ -269,12 +269,12 @@ std::string state_key(Method m, const char *key, const void *src) {
     return key ? std::string(key) : std::string();
 }
 
-// Device-wide admission of fused thresholdv16 kernels.  Each fused launch
-// spin-waits on its own workgroups (count exchange, regime-B barriers), so all
-// of them must be co-resident: with W workgroups per CU at most 2/W fused
-// kernels may be in flight per device.  A launch on stream s first makes s
-// wait for the oldest in-flight fused kernel of another stream when the lane
-// is full (same-stream kernels are already ordered).
+// Device-wide admission of thresholdv16 launches.  No launch waits on a
+// workgroup that is not running (chunks are taken dynamically), so admission
+// is a throughput policy, not a correctness one: STG_TV16_INFLIGHT (1-4,
+// default 1) launches per device share its two 1024-thread workgroup slots
+// per CU; a launch on stream s first makes s wait for the oldest in-flight
+// launch of another stream when the lane is full.
 struct FusedLane {
     std::mutex mu;
     std::vector<std::pair<hipEvent_t, hipStream_t>> inflight;  // oldest first
@@ -282,20 +282,13 @@ struct FusedLane {
 };
 FusedLane g_lanes[64];
 
-// Fused launches co-resident per device (STG_TV16_INFLIGHT, 1-2; the older
-// STG_TV16_WGPERCU=1 means 2).  The device's two 1024-thread workgroup slots
-// per CU are split evenly between them.  Clamped to 2: with 4 launches of 128
-// workgroups in flight (bench --streams 4 --keys 32) some workgroups of a
-// launch were not resident while their peers waited on them -- the bounded
-// waits timed out and stg_codec_check reported spin failures.
 uint32_t fused_inflight() {
     static const uint32_t v = [] {
         if (const char *e = getenv("STG_TV16_INFLIGHT")) {
             const int x = atoi(e);
-            return (uint32_t)std::min(2, std::max(1, x));
+            return (uint32_t)std::min(4, std::max(1, x));
         }
-        const char *e = getenv("STG_TV16_WGPERCU");
-        return (uint32_t)(e && atoi(e) == 1 ? 2 : 1);
+        return 1u;
     }();
     return v;
 }
@@ -323,17 +316,18 @@ int validate(const stg_codec *h, size_t n, uint32_t k, size_t idx_cap, size_t va
 }
 
 // One thresholdv16 launch over `nb` buckets with distinct keys (caller holds
-// ws->mu).  Line-sum scratch is carved per bucket from ws->d.sums.
+// ws->mu).  Scratch is carved per bucket from ws->d.sums: the first-threshold
+// line sums, later the fill's candidate heap (two words per line).
 int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> &grp, hipStream_t s) {
     if (grp.empty()) return STG_OK;
     size_t need = 0;
-    for (auto &b : grp) need += (b.n + 15) / 16 + 64;
+    for (auto &b : grp) need += 2 * ((b.n + 15) / 16 + 64);
     int rc;
     if ((rc = ws->ensure(need, 1, 1))) return rc;
     size_t off = 0, chunks = 0;
     for (auto &b : grp) {
         b.sums = ws->d.sums + off;
-        off += (b.n + 15) / 16 + 64;
+        off += 2 * ((b.n + 15) / 16 + 64);
         chunks += std::max<size_t>(1, (b.n / 16 + stg::TV16_CHUNK - 1) / stg::TV16_CHUNK);
     }
     if ((rc = ws->ensure_desc(chunks))) return rc;
@@ -355,11 +349,16 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     a.epoch = ws->epoch;
     // Workgroups are dealt round-robin over the 8 XCDs (32 CUs, 64 slots
     // each): a launch's share is a multiple of 8 so every XCD holds the same
-    // number of each launch's workgroups and the in-flight launches fit
-    // (170 + 170 + 170 would put 66 on XCD 0 and leave two unresident).
+    // number of each launch's workgroups.
     const uint32_t inflight = fused_inflight();
     constexpr uint32_t XCDS = 8;
-    a.max_wg = std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / inflight * XCDS);
+    // Every launch may use the whole chip (two 1024-thread workgroups per
+    // CU): with dynamic chunk takes, the workgroups of concurrent launches
+    // simply interleave as slots free up (STG_TV16_SHARE=1 splits the slots
+    // evenly between the in-flight launches instead).
+    static const bool share = getenv("STG_TV16_SHARE") && atoi(getenv("STG_TV16_SHARE")) == 1;
+    a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / inflight * XCDS)
+                     : (uint32_t)(2 * h->num_cu);
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     FusedLane &lane = g_lanes[h->device & 63];
     std::lock_guard<std::mutex> lg(lane.mu);
@@ -726,6 +725,18 @@ int stg_codec_check(stg_codec_t h) {
             return fail(STG_ERR_DEVICE, m);
         }
     }
+    return STG_OK;
+}
+
+int stg_codec_debug_words(stg_codec_t h, void *stream, uint32_t *out, int n) {
+    if (!h || !out || n < 0 || n > 64) return fail(STG_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Workspace *ws = nullptr;
+    int rc = h->workspace(s, &ws);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpy(out, ws->d.misc, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return STG_OK;
 }
 

@@ -8,13 +8,9 @@
 
 namespace stg {
 
-constexpr uint32_t TV16_TILE_BLOCKS = 512;   // 16-float lines per scan tile (32 KiB)
-constexpr uint32_t TV16_UNROLL = TV16_TILE_BLOCKS / (STG_WG / 4);  // 8 float4 per lane
-constexpr uint32_t HBINS = 1024;             // regime-B histogram bins per level
-constexpr uint32_t MAX_LEVELS = 6;           // regime-B radix-descent levels
-constexpr uint32_t CAND_CAP = 4096;          // regime-B candidates ranked in LDS per bucket
-constexpr uint32_t SORT_CAP = 16 * CAND_CAP; // global candidate buffers: one per bucket of a launch
-constexpr uint32_t MAX_FILL_WG = 1024;       // upper bound on fill-kernel workgroups
+constexpr uint32_t CAND_CAP = 4096;          // regime-B window entries per bucket (+1 for the ragged tail)
+constexpr uint32_t CAND_WORDS = 4 * CAND_CAP; // per bucket: line-sum bits | line position | candidate index | spare
+constexpr uint32_t TV16_WIN = 1u << 17;      // regime-B window below t, in ulps of t (~1.6 %)
 
 constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)
 constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
@@ -23,60 +19,35 @@ constexpr uint32_t TV_SCAP = 2048;           // threshold-v qualifiers listed pe
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 
 // thresholdv16 in-launch control block (one launch = a batch of <= MAX_BATCH
-// buckets cut into fixed 2048-line chunks).  Per-call counters come in two
-// copies selected by the call epoch's parity; every launch zeroes the other
-// copy for the next call (the next call on this workspace is stream-ordered
-// after this launch).  Words handed between workgroups carry the call tag
-// (epoch << 8 | kind) so stale words of earlier calls never match.
-// Regime-B candidate sets: one CAND_CAP slot per bucket of the launch.
+// buckets cut into fixed 2048-line chunks).  The per-call chunk counter comes
+// in two copies selected by the call epoch's parity; every launch zeroes the
+// other copy for the next call (the next call on this workspace is
+// stream-ordered after this launch).  Words handed between workgroups carry
+// the call tag (epoch << 8 | kind) so stale words of earlier calls never match.
 constexpr uint32_t MAX_BATCH = 16;
 constexpr uint32_t TV16_CHUNK = 2048;        // lines (16 floats) per chunk = 128 KiB
-struct BucketCtl {
-    uint32_t cand_n;    // regime-B candidates appended (rare paths only)
-    uint32_t pad[3];
-    uint32_t hist[MAX_LEVELS][HBINS];
-};
 struct CallCtl {
-    uint32_t bar;       // grid-barrier arrivals (round r completes at r * G)
     uint32_t next;      // dynamic chunk counter
-    uint32_t pad[2];
-    BucketCtl bk[MAX_BATCH];
+    uint32_t pad[31];
 };
-// One 128-byte line per workgroup, written by a barrier's last arriver and
-// polled only by its owner (no line is polled by more than one workgroup).
-struct alignas(128) WgSlot {
-    uint64_t go;        // {epoch tag:32 | barrier round:32}
-    uint64_t pad[15];
-};
-// Per-bucket regime decision, written by the finisher of the bucket's first
-// chunk: [1..3] first, drained, then [0] = {tag:32 | flags:32}.
+// Per-bucket regime decision, written by the finisher of the bucket's last
+// chunk: [1..3] first, drained, then [0] = {tag:32 | flags:32}; read by the
+// follow-on fill launch.
 struct alignas(32) Decision {
     uint64_t w[4];      // [1] = {cnt:32 | M:32}, [2] = {Wtot:32 | tail key bits:32}, [3] = {Qtot:32 | t bits:32}
 };
-// Per-bucket "window lists complete" word {tag:32 | window lines:32}, written
-// by one ranker (the only poller of the list counter the finishers add to) and
-// polled by the rest of its group: one 128-byte line each.
-struct alignas(128) ReadyLine {
-    uint64_t w;
-    uint64_t pad[15];
-};
-// Per-workgroup window-list counts, one 128-byte line per workgroup (no line
-// is written by two workgroups): [b] = {tag:32 | chunks:16 | window lines:16},
-// cumulative over the call, lines saturating at 0xffff.
-struct alignas(128) WgLists {
-    uint64_t w[MAX_BATCH];
-};
+constexpr uint32_t TV16_DEC_B = 1, TV16_DEC_WIN = 2, TV16_DEC_TAIL = 4;  // Decision flags
+constexpr uint32_t TV16_TAG_DEC = 3;
+constexpr uint32_t POISON_COUNT = 0xffffffffu;  // *count_out of a launch that hit a device failure
 struct FillCtl {
     CallCtl cc[2];                     // [epoch parity]
     Decision dec[MAX_BATCH];
-    ReadyLine ready[MAX_BATCH];
-    WgSlot slot[MAX_FILL_WG];
-    WgLists lst[MAX_FILL_WG];
 };
-// Per-chunk descriptor (16 B): every word carries the call tag.
+// Per-chunk descriptor (16 B): {tag:32 | qualifying lines:16 | window lines:16}
+// by the chunk's last streaming wave.
 struct alignas(16) ChunkDesc {
-    uint64_t agg;       // {tag:32 | qualifying lines:16 | window lines:16}, by the last streaming wave
-    uint64_t ties;      // {tag:32 | lines tied at u* (regime-B rare path)}
+    uint64_t agg;
+    uint64_t pad;
 };
 
 // Per-call scalars handed from the scan kernel to the fill kernel.
@@ -103,7 +74,7 @@ struct DevWS {
     CallParams *cp;
     RSel *rsel;
     uint32_t *fail;      // sticky failure bits
-    uint64_t *cand;      // regime-B candidates (key << 32 | pos), CAND_CAP per bucket of a launch
+    uint32_t *cand;      // regime-B window entries, CAND_WORDS per bucket of a launch
     uint32_t *misc;      // small scratch (counts)
     float *sums;         // thresholdv16: one sum per 16-float line
     uint32_t *tile_cnt;  // per-tile qualifier counts
@@ -124,7 +95,8 @@ struct Tv16Bucket {
     uint32_t *count_out;
     KeyState *state;
     bool first;        // no AIMD state yet: compute the first threshold
-    float *sums;       // per-bucket scratch (first threshold; ranges beyond LDS)
+    float *sums;       // per-bucket scratch: first-threshold line sums; the fill's candidate heap
+                       // (2 words per line: (nb + 1) * 2 floats)
     float *resid;      // MERGE error feedback: receives the bucket's full lines, or null
 };
 struct Tv16Launch {
@@ -137,6 +109,26 @@ struct Tv16Launch {
     uint32_t desc_cap;   // ChunkDesc entries at ws.desc
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
+// thresholdv16 regime-B heap fill (tv16fill.hip): one workgroup per bucket
+struct Tv16FillBucket {
+    const float *src;
+    uint32_t *idx;
+    float *val;
+    uint32_t *count_out;
+    uint32_t nb, tl, dst_len;
+    int32_t idx_offset;
+    const uint32_t *cand;  // the bucket's window entries (CAND_WORDS)
+    uint2 *heap;           // full-path scratch: (nb + 1) candidates {key bits, element position}
+};
+struct Tv16FillArgs {
+    Tv16FillBucket bk[MAX_BATCH];
+    uint32_t nbk;
+    uint32_t epoch;
+    const Decision *dec;
+    uint32_t *fail;
+    uint32_t *dbg;         // diagnostics: phase stamps of workgroup 0 (ws.misc)
+};
+hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
 
 struct TvLaunch {
     const float *src;

@@ -8,6 +8,11 @@ def bits(a: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
+def fbits(x) -> int:
+    """Bit pattern of one float32 scalar."""
+    return int(np.float32(x).view(np.uint32))
+
+
 def assert_same_pairs(idx_a, val_a, idx_b, val_b, n: int):
     """Bit-exact equality of the first n (idx, val) pairs as sets (order-free)."""
     ia, ib = np.asarray(idx_a[:n], np.uint32), np.asarray(idx_b[:n], np.uint32)

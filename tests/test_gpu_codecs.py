@@ -10,7 +10,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from parity import assert_same_pairs, assert_same_stream, bits
+from parity import assert_same_stream, bits
 from stellatrain_amd.synth import D1, D2, D3, seed_for, synth
 
 pytestmark = pytest.mark.gpu
@@ -56,9 +56,8 @@ def test_thresholdv16_parity(gpu, oracle, n, k, dist, param):
         cg = comp.compress("3@weight", d, k, idx, val)
         assert cg == co
         ig, vg = idx.cpu().numpy().view(np.uint32), val.cpu().numpy()
-        # the heap fill orders equal sums by libstdc++ heap order (oracle) vs
-        # position (GPU); with distinct sums the streams are identical
-        assert_same_pairs(ig, vg, io, vo, co)
+        # the whole stream, heap fill included (libstdc++ pop order, tv16fill.hip)
+        assert_same_stream(ig, vg, io, vo, co)
         so, sg = oracle.tv16_state(ho, "3@weight"), comp.state("3@weight")
         assert bits(np.array(so, np.float32)).tolist() == bits(np.array(sg, np.float32)).tolist()
         if t_before is not None:
@@ -71,14 +70,14 @@ def test_thresholdv16_parity(gpu, oracle, n, k, dist, param):
 
 @pytest.mark.parametrize("n,k,dist", [(1 << 20, 10485, D1), (100013, 1007, D1), (262144, 2621, D2)])
 def test_thresholdv16_stream_order(gpu, oracle, n, k, dist):
-    """Whole output stream in order: the ordered-scan prefix exactly, the heap
-    fill exactly after canonicalising runs of equal line sums (the only
-    freedom: libstdc++ heap order vs position order among equal sums)."""
+    """Whole output stream in order, bit-exact: the ordered-scan prefix and the
+    heap fill in libstdc++ priority_queue pop order (equal line sums occur in
+    most regime-B calls of D1 data)."""
     import torch
-    from parity import canonical_heap_order
     from stellatrain_amd import ThresholdvCompressor16
     comp = ThresholdvCompressor16()
     ho = oracle.tv16_new()
+    tied_fills = 0
     for it in range(8):
         src = synth(n, seed_for(1, it), dist)
         t_before = oracle.tv16_state(ho, "k")
@@ -88,18 +87,20 @@ def test_thresholdv16_stream_order(gpu, oracle, n, k, dist):
         assert comp.compress("k", torch.from_numpy(src).to(gpu), k, idx, val) == co
         ig, vg = idx.cpu().numpy().view(np.uint32), val.cpu().numpy()
         head = _regime_split(oracle, src, k, t_before[0], co) if t_before is not None else 0
-        assert_same_stream(ig, vg, io, vo, head)
-        a_i, a_v = canonical_heap_order(ig, vg, head, co, src, oracle)
-        b_i, b_v = canonical_heap_order(io, vo, head, co, src, oracle)
-        assert_same_stream(a_i, a_v, b_i, b_v, co)
+        assert_same_stream(ig, vg, io, vo, co)
+        sums = oracle.tv16_block_sums(src)
+        if t_before is not None and head < co:
+            ties = np.unique(sums[np.asarray(io[head:co:16], np.int64) // 16 % sums.size], return_counts=True)[1]
+            tied_fills += int((ties > 1).any())
+    if n == 1 << 20:
+        assert tied_fills  # equal line sums inside the heap fill were exercised
 
 
-@pytest.mark.parametrize("n,k,zp", [(100013, 1007, 9000), (65536, 655, 9995), (1000, 16, 9995)])
+@pytest.mark.parametrize("n,k,zp", [(100013, 1007, 9000), (65536, 655, 9995), (1000, 16, 9995), (1 << 20, 10485, 9995)])
 def test_thresholdv16_ties_sparse(gpu, oracle, n, k, zp):
-    """D3: exact-zero lines tie at sum 0.  Counts, thresholds, the ordered-scan
-    prefix and the multiset of selected line sums and values are exact; which
-    of several zero-sum lines fill the tail follows position order on the GPU
-    and libstdc++ heap order in the reference."""
+    """D3: exact-zero lines tie at sum 0 (99.95 % zeros: the fill reaches
+    into them, so the tie sits at the cut and decides the index SET).  The
+    whole stream equals the reference's: libstdc++ heap order among ties."""
     import torch
     from stellatrain_amd import ThresholdvCompressor16
     comp = ThresholdvCompressor16()
@@ -114,9 +115,7 @@ def test_thresholdv16_ties_sparse(gpu, oracle, n, k, zp):
         ig, vg = idx.cpu().numpy().view(np.uint32), val.cpu().numpy()
         so, sg = oracle.tv16_state(ho, "z"), comp.state("z")
         assert np.float32(so[0]) == np.float32(sg[0]) and np.float32(so[1]) == np.float32(sg[1])
-        np.testing.assert_array_equal(np.sort(bits(vg[:co])), np.sort(bits(vo[:co])))
-        head = _regime_split(oracle, src, k, t_before[0], co) if t_before is not None else 0
-        assert_same_stream(ig, vg, io, vo, head)
+        assert_same_stream(ig, vg, io, vo, co)
         assert np.all(vg[:co] == src[ig[:co]])
         assert len(np.unique(ig[:co])) == co
     comp.check_device()
@@ -217,7 +216,7 @@ def test_host_path_matches_device(gpu, oracle):
         idx = np.zeros(k, np.uint32)
         val = np.zeros(k, np.float32)
         assert comp.compress("h", src, k, idx, val, 5) == co
-        assert_same_pairs(idx, val, io, vo, co)
+        assert_same_stream(idx, val, io, vo, co)
 
 
 # Batched launches: several buckets (distinct keys, mixed sizes incl. buckets
@@ -266,9 +265,7 @@ def test_thresholdv16_batch(gpu, oracle, layout):
         for j, ((key, _, k, idx, val, off), (src, co, io, vo, t_before, _)) in enumerate(zip(items, ref)):
             assert counts[j] == co, (it, j)
             ig, vg = idx.cpu().numpy().view(np.uint32), val.cpu().numpy()
-            assert_same_pairs(ig, vg, io, vo, co)
-            head = _regime_split(oracle, src, k, t_before[0], co) if t_before is not None else 0
-            assert_same_stream(ig, vg, io, vo, head)
+            assert_same_stream(ig, vg, io, vo, co)
         # final state of every key equals the oracle's after its last call
         last = {}
         for (key, *_), r in zip(spec, ref):
@@ -314,7 +311,7 @@ def test_thresholdv16_batch_64mib(gpu, oracle):
             t_before = oracle.tv16_state(ho, keys[i])
             co, io, vo = oracle.tv16_compress(ho, keys[i], srcs[i], k)
             ig, vg = outs[i][0].cpu().numpy().view(np.uint32), outs[i][1].cpu().numpy()
-            assert_same_pairs(ig, vg, io, vo, co)
+            assert_same_stream(ig, vg, io, vo, co)
             so = oracle.tv16_state(ho, keys[i])
             assert bits(np.array(so, np.float32)).tolist() == bits(np.array(comp.state(keys[i]), np.float32)).tolist()
             if t_before is not None:
@@ -326,13 +323,11 @@ def test_thresholdv16_batch_64mib(gpu, oracle):
 
 @pytest.mark.parametrize("n,k,dist,param", [((1 << 21) + 5, 209715, D1, 0), (1 << 20, 1 << 17, D3, 9000)])
 def test_thresholdv16_large_fill(gpu, oracle, n, k, dist, param):
-    """Regime B with far more lines to fill than one rank piece holds
-    (CAND_CAP - 1 = 4095): the inputs' scale drops 100x between calls, so the
-    ordered scan finds almost nothing above the threshold and the heap fill
-    emits up to k/16 lines in several pieces.  D3 adds exact-zero ties that
-    reach past the pieces."""
+    """Regime B far from the window: the inputs' scale drops 100x between
+    calls, so the ordered scan finds almost nothing above the threshold and
+    the heap fill (tv16fill.hip full path: the literal make_heap / pop_heap)
+    emits up to k/16 lines.  D3 adds exact-zero ties at the cut."""
     import torch
-    from parity import canonical_heap_order
     from stellatrain_amd import ThresholdvCompressor16
     comp = ThresholdvCompressor16()
     ho = oracle.tv16_new()
@@ -348,17 +343,9 @@ def test_thresholdv16_large_fill(gpu, oracle, n, k, dist, param):
         so, sg = oracle.tv16_state(ho, "f"), comp.state("f")
         assert bits(np.array(so, np.float32)).tolist() == bits(np.array(sg, np.float32)).tolist(), it
         head = _regime_split(oracle, src, k, t_before[0], co) if t_before is not None else 0
-        if t_before is not None and (co - head) // 16 > 4095:
+        if t_before is not None and (co - head) // 16 > 4095:  # more than the window path could hold
             big += 1
-        assert_same_stream(ig, vg, io, vo, head)
-        if dist == D3:  # which zero-sum lines fill the tail: position vs heap order
-            np.testing.assert_array_equal(np.sort(bits(vg[:co])), np.sort(bits(vo[:co])))
-            assert np.all(vg[:co] == src[ig[:co]])
-            assert len(np.unique(ig[:co])) == co
-        else:
-            a_i, a_v = canonical_heap_order(ig, vg, head, co, src, oracle)
-            b_i, b_v = canonical_heap_order(io, vo, head, co, src, oracle)
-            assert_same_stream(a_i, a_v, b_i, b_v, co)
+        assert_same_stream(ig, vg, io, vo, co)
     comp.check_device()
     oracle.tv16_free(ho)
     assert big  # at least one call filled more than one piece
