@@ -6,10 +6,10 @@ N = 1 (the headline, BASELINE.json metric on configs[1]'s bucket size): one
 16 keys ("<layer>@weight") x 64 MiB fp32 (n = 16,777,216, dst_len = 167,772 =
 merge_numel(n, 0.99)), device resident.  The engine issues its MERGE-compress
 tasks from several pool workers at once (engine/modules/compress.cpp:141,
-config.h:7); here the step is two batched C-ABI calls
-(stg_codec_compress_batch_device) of 8 buckets each on two streams = two
-concurrent persistent launches, so one launch's exchange tail overlaps the
-other's streaming.  Each rank holds 2 buffer sets (the engine's iter%2 shm
+config.h:7); here the step is four batched C-ABI calls
+(stg_codec_compress_batch_device) of 4 buckets each on four streams = four
+concurrent persistent launches, so one launch's tail and regime-B heap fill
+overlap the others' streaming.  Each rank holds 2 buffer sets (the engine's iter%2 shm
 buffers, core.cpp:967) = 32 distinct buckets (2 GiB >> the 256 MB Infinity
 Cache); step s compresses set s%2, so every key sees fresh data each visit and
 its AIMD threshold runs its real regime A/B sequence.  Keys are initialised
@@ -20,7 +20,7 @@ log-uniform, seeded: shard.c4_sizes) sharded over the N ranks by
 shard.ShardPlan (key-affine, bytes-balanced).  Buckets are independent
 (core.cpp:1052-1087), so each rank compresses its own buckets with no
 collective on the data path; one step = one sweep over the rank's buckets in
-batched launches of <= 16 on two streams.  The whole list is fixed, so this is
+batched launches of <= 16 on four streams.  The whole list is fixed, so this is
 strong scaling; value = all ranks' bytes / the slowest rank's time.  RCCL is
 used only for the timing barrier and the max-reduce of the elapsed time.
 
@@ -76,7 +76,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-steps", type=int, default=64)
     p.add_argument("--warmup-seconds", type=float, default=2.0)
-    p.add_argument("--streams", type=int, default=2,
+    p.add_argument("--streams", type=int, default=4,
                    help="issue batch j on stream j %% S, like the engine's worker pool; S persistent launches "
                         "share the chip")
     p.add_argument("--master-port", type=int, default=29517)
@@ -320,7 +320,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt.item())
     comp.check_device()
-    assert bool((counts[:nb].cpu().numpy() == np.array(ks, np.int32)).all()), "count != dst_len"
+    if not os.environ.get("STG_DEBUG_TV16_STAGE"):  # diagnostic stages skip the fill
+        assert bool((counts[:nb].cpu().numpy() == np.array(ks, np.int32)).all()), "count != dst_len"
 
     # ---- live kernel timing (HIP events, no per-launch instrumentation) ----
     # events on stream 0 bracketing the profile steps of all streams: with S

@@ -271,15 +271,29 @@ std::string state_key(Method m, const char *key, const void *src) {
 
 // Device-wide admission of thresholdv16 launches.  No launch waits on a
 // workgroup that is not running (chunks are taken dynamically), so admission
-// is a throughput policy, not a correctness one: STG_TV16_INFLIGHT (1-4,
-// default 1) launches per device share its two 1024-thread workgroup slots
-// per CU; a launch on stream s first makes s wait for the oldest in-flight
-// launch of another stream when the lane is full.
+// is a throughput policy, not a correctness one.
+//  * STG_TV16_SERIAL=1 runs scans one at a time per device: a launch's scan
+//    kernel waits for the previous launch's scan when that was on another
+//    stream, so the previous launch's fill workgroups (which fit beside two
+//    scan workgroups on a CU) run under the next scan.  Off by default: the
+//    event hand-off between streams costs more than it hides, and launches
+//    from three or four streams overlap each other's tails and fills anyway
+//    (profiles/r02_streams.jsonl).
+//  * STG_TV16_INFLIGHT (1-4, default 1) launches per device in flight: a
+//    launch on stream s first makes s wait for the oldest in-flight launch of
+//    another stream when the lane is full.
 struct FusedLane {
     std::mutex mu;
     std::vector<std::pair<hipEvent_t, hipStream_t>> inflight;  // oldest first
     std::vector<hipEvent_t> pool;
+    hipEvent_t scan_ev = nullptr;  // recorded after the last launch's scan
+    hipStream_t scan_stream = nullptr;
 };
+
+bool tv16_serial() {
+    static const bool v = getenv("STG_TV16_SERIAL") && atoi(getenv("STG_TV16_SERIAL")) == 1;
+    return v;
+}
 FusedLane g_lanes[64];
 
 uint32_t fused_inflight() {
@@ -352,8 +366,8 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     // number of each launch's workgroups.
     const uint32_t inflight = fused_inflight();
     constexpr uint32_t XCDS = 8;
-    // Every launch may use the whole chip (two 1024-thread workgroups per
-    // CU): with dynamic chunk takes, the workgroups of concurrent launches
+    // Every launch may use the whole chip (two scan workgroups per CU): with
+    // dynamic chunk takes, the workgroups of concurrent launches
     // simply interleave as slots free up (STG_TV16_SHARE=1 splits the slots
     // evenly between the in-flight launches instead).
     static const bool share = getenv("STG_TV16_SHARE") && atoi(getenv("STG_TV16_SHARE")) == 1;
@@ -368,6 +382,12 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
         lane.inflight.erase(lane.inflight.begin());
         if (old.second != s) HIP_TRY(hipStreamWaitEvent(s, old.first, 0));
         lane.pool.push_back(old.first);
+    }
+    if (tv16_serial()) {
+        if (lane.scan_ev && lane.scan_stream != s) HIP_TRY(hipStreamWaitEvent(s, lane.scan_ev, 0));
+        if (!lane.scan_ev) HIP_TRY(hipEventCreateWithFlags(&lane.scan_ev, hipEventDisableTiming));
+        a.scan_done = lane.scan_ev;  // a wait enqueued above keeps the record it saw
+        lane.scan_stream = s;
     }
     HIP_TRY(stg::launch_tv16(a, ws->d, s));
     hipEvent_t done;

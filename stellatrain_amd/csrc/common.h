@@ -43,14 +43,17 @@ constexpr int QP_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-// Wave-wide inclusive scan of a uint32 (64 lanes).
+// Wave-wide inclusive scan of a uint32 (64 lanes) on DPP: row shifts by 1,
+// 2, 4, 8 (lanes shifted in from outside the row of 16 add 0), then the row
+// broadcasts of lanes 15 and 31 into the rows above.  No LDS, no address
+// registers (the ds_bpermute form keeps six lane offsets live).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const uint32_t lane = __lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t)d) v += o;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 

@@ -13,11 +13,11 @@
 // t *= 0.99 (in double) when the scan ran dry, t += inc otherwise.
 //
 // One persistent launch per batch of buckets (tv16_batch).  The buckets are
-// cut into 2048-line chunks (128 KiB), taken in order by 1024-thread
-// workgroups from a per-call counter -- every slot, the first two included --
+// cut into 2048-line chunks (128 KiB), taken in order by 768-thread
+// workgroups (two per CU) from a per-call counter -- every slot, the first two included --
 // so fast workgroups take more chunks and every wait below points at a chunk
 // an already-running workgroup has taken: the launch needs no workgroup to be
-// co-resident with any other.  The 16 waves of a workgroup are specialised:
+// co-resident with any other.  The 12 waves of a workgroup are specialised:
 //
 //   streaming waves  scan chunk after chunk and never wait on another
 //             workgroup: stream the chunk once (a quad of lanes per line, DPP
@@ -53,14 +53,14 @@ using namespace tv16;
 #define STG_EF_AUX 2  // cache policy of the fused residual stores (2: nontemporal)
 #endif
 
-constexpr uint32_t FWG = 1024;      // workgroup: 16 waves
-constexpr uint32_t FNW = FWG / 64;
 #ifndef STG_TV16_NS
-#define STG_TV16_NS 15
+#define STG_TV16_NS 11
 #endif
+constexpr uint32_t FWG = (STG_TV16_NS + 1) * 64;  // workgroup: the streaming waves + the finisher
+constexpr uint32_t FNW = FWG / 64;
 constexpr uint32_t NS = STG_TV16_NS;  // streaming waves 0..NS-1
 constexpr uint32_t FIN = NS;          // the finisher; waves past it (if any) idle
-static_assert(NS + 1 <= FNW, "streaming group + finisher fit the workgroup");
+static_assert(NS + 1 <= FNW && FWG <= 1024, "streaming group + finisher fit the workgroup");
 #ifndef STG_TV16_NBUF
 #define STG_TV16_NBUF 5
 #endif
@@ -178,6 +178,7 @@ struct Lds {
     // finisher
     uint4 gb[GB];                        // gathered chunk descriptors (one piece of a bucket)
 };
+static_assert(sizeof(Lds) <= TV16_SCAN_LDS, "two scan workgroups and a fill workgroup share a CU");
 
 // Spin-timeout failure bits: FAIL_SPIN_TIMEOUT plus bit 8 + site naming the
 // wait that gave up: 1 buffer set, 2 prefix aggregates, 3 chunk streamed,
@@ -652,7 +653,13 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k) {
 // streaming waves' work only (the finisher releases buffers at once);
 // 3 = plain streaming read (calibration).
 template <int STAGE, bool EF>
-__global__ void __launch_bounds__(FWG, 8) tv16_batch(BatchArgs A) {
+// Registers for 8 waves per SIMD (<= 64 VGPRs): two workgroups per CU take 6
+// waves per SIMD and a fill workgroup's 2 run beside them.  The bound says
+// 1024 threads (launches use FWG <= 1024) so that the compiler, which derives
+// the occupancy it aims for from the bound, does not widen the register
+// budget to the 6 waves two FWG-thread workgroups would give.
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+tv16_batch(BatchArgs A) {
     __shared__ Lds L;
     Ctx C{A, L, gridDim.x, blockIdx.x, A.ctl, A.cand, A.fail};
     {  // zero the next call's per-call counters (this call never touches them)
@@ -768,7 +775,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     A.desc = ws.desc;
     A.cand = ws.cand;
     A.fail = ws.fail;
-    // this launch's share of the device's two 1024-thread workgroups per CU
+    // this launch's share of the device's two scan workgroups per CU
     // (all of them for one stream; launches from several streams split them);
     // no more than there are chunks.  Co-residency is not required.
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(a.max_wg, K), MAXG));
@@ -783,6 +790,10 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             break;
     }
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
+    if (a.scan_done) {
+        const hipError_t e = hipEventRecord(a.scan_done, s);
+        if (e != hipSuccess) return e;
+    }
     if (dbg_stage != 1 && dbg_stage != 3) {
         // regime-B heap fill: one workgroup per bucket, stream-ordered after the scan
         F.nbk = a.nb;
@@ -790,6 +801,9 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.dec = ws.ctl->dec;
         F.fail = ws.fail;
         F.dbg = ws.misc;
+        static const uint32_t fill_mode =
+            getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
+        F.mode = fill_mode;
         const hipError_t e = launch_tv16_fill(F, s);
         if (e != hipSuccess) return e;
     }

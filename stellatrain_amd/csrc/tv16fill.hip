@@ -28,6 +28,20 @@
 //      for R, and the pop sequence of a heap is root, then the merge of its
 //      subtrees' sequences with ties going to the right subtree -- i.e. R in
 //      (sum desc, right-first pre-order of its make_heap position) order.
+//  (3) Without the heap: an element leaves the subtree of its start node
+//      only upwards, through its ancestors (it moves down only as the value
+//      of its own sift, inside that subtree), and a node takes the larger of
+//      its children's entries, the right one on equal sums, from subtrees
+//      that are heaps by then.  So of two equal sums a, b whose start nodes
+//      are not one above the other, the one on the right side of their
+//      lowest common ancestor passes it first (the other side's entry is
+//      >= the other element), and they keep that order above it, through
+//      the pops.  Hence when no two equal sums among the pops start one
+//      above the other, they pop in right-first pre-order of their START
+//      positions; and when no element of R starting in the last P + 1
+//      positions has an R element at its parent or sibling, each of them
+//      has moved up before the pops begin, so (2) holds.  Both are checked
+//      (a few thousand comparisons); almost every regime-B call ends here.
 // Full path (otherwise: the window missed the top M, > 4096 entries, or a
 // bucket of 2^20+ lines): the candidate vector is built in global memory and
 // make_heap / pop_heap run literally (make_heap level-parallel: subtrees of
@@ -43,14 +57,22 @@ namespace {
 
 using namespace tv16;
 
-constexpr uint32_t FILL_WG = 1024;
-constexpr uint32_t EMAX = CAND_CAP;            // R: window entries + the ragged tail
+constexpr uint32_t FILL_WG = 512;              // 8 waves: beside two 12-wave scan workgroups
+constexpr uint32_t FNW_F = FILL_WG / 64;
+constexpr uint32_t EMAX = CAND_CAP;            // window entries + the ragged tail
 constexpr uint32_t VCAP = 6144;                // shadow-heap nodes held (more: full path)
-constexpr uint32_t DMAX = 20;                  // depths 0..19: positions < 2^20 - 1
 constexpr uint32_t POS_LIM = (1u << 20) - 1;   // fast path: N <= POS_LIM (20-bit paths)
 constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint16_t NONE16 = 0xffffu;
-constexpr uint32_t NBIN = 2048;                // counting-sort bins
+constexpr uint32_t NONE13 = 0x1fffu;           // no node (13-bit node index)
+constexpr uint32_t CNONE = 0xffffffu;          // content -inf (24-bit content field)
+constexpr uint32_t NBIN = 1024;                // counting-sort bins
+constexpr uint32_t NDEP = 20;                  // depths 0..19
+constexpr uint32_t PT = EMAX / FILL_WG;        // ranks / DFS slots per thread
+constexpr uint32_t NJ = VCAP / FILL_WG;        // nodes per thread
+constexpr uint32_t TCAP = 256;                 // tied ranks checked without the heap (more: the heap)
+constexpr uint32_t ECAP = 64;                  // late start positions checked (more: the heap)
+static_assert(VCAP < NONE13, "13-bit node indices");
+static_assert(NBIN << 7 == TV16_WIN, "output-sort bins of 128 ulps cover the window");
 
 // A heap node as a DFS key: its path from the root left-aligned to depth 19
 // (20 bits) << 5 | its depth.  Ascending keys = pre-order, left subtree first;
@@ -69,10 +91,6 @@ __device__ __forceinline__ uint32_t dk_left(uint32_t k) { return (k & ~31u) | (d
 __device__ __forceinline__ uint32_t dk_right(uint32_t k) {
     return (((k >> 5) | (1u << (18u - dk_depth(k)))) << 5) | (dk_depth(k) + 1);
 }
-__device__ __forceinline__ uint32_t dk_parent(uint32_t k) {
-    const uint32_t d = dk_depth(k);
-    return (((k >> 5) & ~(1u << (19u - d))) << 5) | (d - 1);
-}
 // depth of the lowest common ancestor of two nodes (DFS keys)
 __device__ __forceinline__ int dk_lca(uint32_t a, uint32_t b) {
     const uint32_t m = min(dk_depth(a), dk_depth(b));
@@ -80,46 +98,77 @@ __device__ __forceinline__ int dk_lca(uint32_t a, uint32_t b) {
     return x ? (int)m - (int)(32u - __clz(x)) : (int)m;
 }
 
+// A shadow-heap node record (8 bytes, one ds_read_b64):
+//   .x = content (grp << 12 | rank; CNONE: -inf) | pos[7:0] << 24
+//   .y = pos[19:8] | right child << 12 | has left << 25 | has right << 26 | U << 27
+// The left child, when present, is the next node in pre-order.
+__device__ __forceinline__ uint32_t r_content(uint2 r) { return r.x & CNONE; }
+__device__ __forceinline__ uint32_t r_pos(uint2 r) { return (r.x >> 24) | ((r.y & 0xfffu) << 8); }
+__device__ __forceinline__ uint32_t r_right(uint2 r) { return (r.y >> 12) & NONE13; }
+__device__ __forceinline__ bool r_hasl(uint2 r) { return (r.y >> 25) & 1u; }
+__device__ __forceinline__ bool r_hasr(uint2 r) { return (r.y >> 26) & 1u; }
+__device__ __forceinline__ bool r_isu(uint2 r) { return (r.y >> 27) & 1u; }
+__device__ __forceinline__ uint2 r_make(uint32_t content, uint32_t pos, bool isu) {
+    return make_uint2(content | (pos << 24), (pos >> 8) | (isu ? 1u << 27 : 0u));
+}
+
 struct SortScratch {
     uint32_t bin[NBIN];  // counts -> starts
     uint32_t cur[NBIN];  // scatter cursors
-    uint16_t tmp[VCAP];  // items grouped by bin
-    uint16_t ord[VCAP];  // the sorted order
+    uint16_t tmp[EMAX];  // items grouped by bin
 };
 
-// LDS of a fill workgroup (< 124 KiB: it shares a CU with one scan workgroup).
+// LDS of a fill workgroup: it runs beside two scan workgroups on one CU.
+// Elements are window entries (ids < W); ranks are positions in the output
+// order `ord`; R, the shadow heap's elements, are the ranks [0, rn).  The
+// union's views follow the phases; each is written only after a barrier that
+// ends every read of what it covers.
 struct FillLds {
-    uint32_t key[EMAX];   // line-sum bits (the tail: its signed key's bits)
-    uint32_t cix[EMAX];   // candidate index -> start node (DFS key) -> final position
+    uint16_t ord[EMAX];  // rank -> element: (sum desc, position asc), then ties in heap order
+    uint16_t grp[EMAX];  // rank -> first rank of its equal-sum run
     union {
-        struct {                   // element DFS order, then shadow-heap node construction
-            uint32_t vlist[VCAP];  // nodes (DFS keys), unsorted
-            SortScratch s;         // element order, then node order
+        struct {  // load and output sort
+            uint32_t key[EMAX];   // element -> line-sum bits (the tail: its signed key's bits)
+            uint32_t cix[EMAX];   // element -> candidate index (= start heap position)
+            SortScratch s;
+            uint32_t line[EMAX];  // element -> first element of its line (the emission; V goes over it)
         } a;
-        struct {                   // the shadow heap: nodes in DFS order
-            uint16_t vc[VCAP];     // element at the node (NONE16: -inf)
-            uint16_t vr[VCAP];     // right child's node index (NONE16: -inf)
-            uint32_t vk[VCAP];     // the node's DFS key
-            uint16_t ord_spare[VCAP];
-            uint16_t ulist[VCAP];  // nodes with a child in the heap, by depth
-        } h;
-        SortScratch o;             // output order
-    } r;
-    uint32_t uoff[DMAX + 2];
-    uint32_t sh[32];      // block-scan scratch
-    uint32_t flag, nv, maxpos, npop;
+        struct {  // DFS sort of R
+            uint32_t dk[EMAX];  // rank -> DFS key of its start position (over key)
+            uint16_t eo[EMAX];  // ranks in DFS order (over cix)
+            uint16_t pad[EMAX];
+            SortScratch s;
+        } b;
+        struct {  // the nodes V in pre-order (over dk / eo: built from registers)
+            uint32_t vk[VCAP];    // DFS key
+            uint2 rec[VCAP + 1];  // [VCAP]: a -inf leaf, read in place of a missing node
+        } v;
+        struct {  // the sift
+            uint16_t ul[VCAP];  // U nodes by depth, deepest first (over vk)
+            uint16_t pad[VCAP];
+            uint2 rec[VCAP + 1];
+        } w;
+        struct {  // the tie order
+            uint32_t fpos[EMAX];  // rank -> final heap position (over ul)
+            uint16_t ord2[EMAX];
+        } f;
+    } u;
+    uint32_t sh[32];  // block-scan scratch
+    uint32_t cnt[NDEP + 1], uoff[NDEP + 1];
+    uint16_t tl[TCAP];  // tied ranks among the pops
+    uint32_t el[ECAP];  // start positions of R among the last P + 1
+    uint32_t flag, nv, maxpos, npop, dmax, rn, nc, nu, ntl, nel, flag2;
 };
-static_assert(sizeof(FillLds) <= 120 * 1024, "a fill workgroup beside one scan workgroup per CU");
-static_assert(offsetof(FillLds, r) + offsetof(decltype(FillLds::r), h.vk) >=
-              offsetof(FillLds, r) + offsetof(decltype(FillLds::r), a.s.bin), "vk is written over the node sort's bins");
+static_assert(sizeof(FillLds) + 2 * TV16_SCAN_LDS <= 160 * 1024, "a fill workgroup beside two scan workgroups");
+static_assert(EMAX <= 4096, "ranks fit the 12-bit content fields");
+static_assert(sizeof(uint32_t) * EMAX + sizeof(uint16_t) * EMAX <= sizeof(uint32_t) * VCAP,
+              "the tie order stays clear of the node records");
 
-__device__ __forceinline__ float kf(const FillLds &S, uint32_t e) { return e == NONE ? -INFINITY : u2f(S.key[e]); }
-
-// Counting sort of items 0..n-1 by (bin(i), full(i)) ascending into X.ord:
+// Counting sort of items 0..n-1 by (bin(i), full(i)) ascending into out:
 // bins of a few items each; inside a bin, an item's rank is the number of
 // bin members with a smaller full key.
 template <typename Bin, typename Full>
-__device__ void counting_sort(SortScratch &X, uint32_t *sh, uint32_t n, Bin bin_of, Full full_of) {
+__device__ void counting_sort(SortScratch &X, uint16_t *out, uint32_t *sh, uint32_t n, Bin bin_of, Full full_of) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < NBIN; i += FILL_WG) X.bin[i] = 0;
     __syncthreads();
@@ -127,10 +176,10 @@ __device__ void counting_sort(SortScratch &X, uint32_t *sh, uint32_t n, Bin bin_
     __syncthreads();
     {  // exclusive scan of the bins, NBIN / FILL_WG per thread
         constexpr uint32_t PER = NBIN / FILL_WG;
-        uint32_t c0 = X.bin[PER * tid], c1 = X.bin[PER * tid + 1];
         static_assert(PER == 2, "two bins per thread");
+        const uint32_t c0 = X.bin[PER * tid], c1 = X.bin[PER * tid + 1];
         uint32_t tot;
-        const uint32_t run = blk_excl_scan<FILL_WG / 64>(c0 + c1, sh, &tot);
+        const uint32_t run = blk_excl_scan<FNW_F>(c0 + c1, sh, &tot);
         X.bin[PER * tid] = X.cur[PER * tid] = run;
         X.bin[PER * tid + 1] = X.cur[PER * tid + 1] = run + c0;
     }
@@ -142,65 +191,9 @@ __device__ void counting_sort(SortScratch &X, uint32_t *sh, uint32_t n, Bin bin_
         const uint64_t k = full_of(e);
         uint32_t r = lo;
         for (uint32_t x = lo; x < hi; ++x) r += full_of(X.tmp[x]) < k;
-        X.ord[r] = (uint16_t)e;
+        out[r] = (uint16_t)e;
     }
     __syncthreads();
-}
-
-// index of DFS key k among the sorted node keys vk[0..nv), or NONE16
-__device__ __forceinline__ uint32_t vfind(const FillLds &S, uint32_t nv, uint32_t k) {
-    uint32_t lo = 0, hi = nv;
-    while (lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (S.r.h.vk[m] < k) lo = m + 1; else hi = m;
-    }
-    return lo < nv && S.r.h.vk[lo] == k ? lo : NONE16;
-}
-__device__ __forceinline__ uint32_t vleft(const FillLds &S, uint32_t nv, uint32_t v) {
-    return v + 1 < nv && S.r.h.vk[v + 1] == dk_left(S.r.h.vk[v]) ? v + 1 : NONE16;
-}
-__device__ __forceinline__ uint32_t velem(const FillLds &S, uint32_t v) {
-    if (v == NONE16) return NONE;
-    const uint32_t e = S.r.h.vc[v];
-    return e == NONE16 ? NONE : e;
-}
-
-// libstdc++ __adjust_heap (heap length N) at shadow-heap node v; the descent
-// stops where both children are -inf (nothing below moves an element of R).
-__device__ void shadow_sift(FillLds &S, uint32_t nv, uint32_t v, uint32_t N) {
-    const uint32_t x = velem(S, v);
-    uint32_t hole = v, hpos = dk_pos(S.r.h.vk[v]);
-    bool entered = false;
-    const uint32_t half = (N - 1) / 2;
-    while (hpos < half) {  // while (secondChild < (len - 1) / 2), secondChild == the hole
-        const uint32_t r = S.r.h.vr[hole], l = vleft(S, nv, hole);
-        uint32_t er = velem(S, r == NONE16 ? NONE16 : r);
-        const uint32_t el = velem(S, l);
-        uint32_t c = r, cpos = 2 * (hpos + 1);
-        if (kf(S, er) < kf(S, el)) { c = l; er = el; --cpos; }
-        if (er == NONE) { entered = true; break; }
-        S.r.h.vc[hole] = (uint16_t)er;
-        hole = c;
-        hpos = cpos;
-    }
-    if (!entered && (N & 1u) == 0 && hpos == (N - 2) / 2) {
-        const uint32_t l = vleft(S, nv, hole);
-        const uint32_t el = velem(S, l);
-        if (el != NONE) { S.r.h.vc[hole] = (uint16_t)el; hole = l; }
-    }
-    if (x == NONE) {  // -inf value: it stays below; the hole's stale copy goes
-        if (hole != v) S.r.h.vc[hole] = NONE16;
-        return;
-    }
-    const float xk = kf(S, x);
-    while (hole != v) {  // __push_heap up to the top index v
-        const uint32_t par = vfind(S, nv, dk_parent(S.r.h.vk[hole]));
-        const uint32_t ep = velem(S, par);
-        if (!(kf(S, ep) < xk)) break;
-        S.r.h.vc[hole] = (uint16_t)ep;
-        hole = par;
-    }
-    S.r.h.vc[hole] = (uint16_t)x;
 }
 
 // right-first pre-order key of heap position pos (< 2^20 - 1): ancestors
@@ -212,67 +205,51 @@ __device__ __forceinline__ uint32_t rf_key(uint32_t pos) {
     return ((inv << (19u - d)) << 5) | d;
 }
 
-// Emit the lines / tail of the output order: element i of the order goes to
+// Emit the lines / tail of the output order: entry i of the order goes to
 // offset cnt + 16 i (less 16 - tl after the tail), at most rem elements.  Four
-// lanes per line (a float4 each), 256 lines per round, loads of four rounds
-// issued before their stores.
-struct EmitEnt {
-    float4 x;
-    uint32_t pos, off, len;
-    bool v4;
-};
-
-template <typename GetPos>
-__device__ __forceinline__ void emit_load(const Tv16FillBucket &d, uint32_t i, uint32_t np, uint32_t rem,
-                                          uint32_t tail_rank, bool vec, GetPos &pos_of, EmitEnt &E) {
-    const uint32_t q = threadIdx.x & 3u;
-    E.len = 0;
-    if (i >= np) return;
-    const bool is_tail = i == tail_rank;
-    E.off = 16u * i - (tail_rank < i ? 16u - d.tl : 0u);
-    if (E.off >= rem) return;
-    E.len = min(is_tail ? d.tl : 16u, rem - E.off);
-    E.pos = pos_of(i);
-    E.v4 = vec && E.len == 16 && (E.off & 3u) == 0;
-    if (E.v4) E.x = *reinterpret_cast<const float4 *>(d.src + (size_t)E.pos + 4 * q);
-}
-
-__device__ __forceinline__ void emit_store(const Tv16FillBucket &d, uint32_t cnt, const EmitEnt &E) {
-    const uint32_t q = threadIdx.x & 3u;
-    if (!E.len) return;
-    const uint32_t o = cnt + E.off + 4 * q, bi = E.pos + 4 * q + (uint32_t)d.idx_offset;
-    if (E.v4) {
-        *reinterpret_cast<float4 *>(d.val + o) = E.x;
-        *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
-        return;
-    }
-    for (uint32_t c = 0; c < 4; ++c) {
-        if (4 * q + c < E.len) {
-            d.val[o + c] = d.src[(size_t)E.pos + 4 * q + c];
-            d.idx[o + c] = bi + c;
-        }
-    }
-}
-
-// Emit the lines / tail of the output order: element i of the order goes to
-// offset cnt + 16 i (less 16 - tl after the tail), at most rem elements.  Four
-// lanes per line (a float4 each), 256 lines per round, the loads of four
-// rounds issued before their stores.
+// lanes per line (a float4 each: one 64-byte request per line), eight rounds
+// of loads in flight before their stores.
 template <typename GetPos>
 __device__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np, uint32_t tail_rank,
                            GetPos pos_of) {
+    constexpr uint32_t K = 5, LPR = FILL_WG / 4;  // rounds in flight, lines per round
     const bool vec = aligned16(d) && (cnt & 3u) == 0;
-    constexpr uint32_t PER = FILL_WG / 4;
-    for (uint32_t i0 = threadIdx.x >> 2; i0 < np; i0 += 4 * PER) {
-        EmitEnt e0, e1, e2, e3;
-        emit_load(d, i0, np, rem, tail_rank, vec, pos_of, e0);
-        emit_load(d, i0 + PER, np, rem, tail_rank, vec, pos_of, e1);
-        emit_load(d, i0 + 2 * PER, np, rem, tail_rank, vec, pos_of, e2);
-        emit_load(d, i0 + 3 * PER, np, rem, tail_rank, vec, pos_of, e3);
-        emit_store(d, cnt, e0);
-        emit_store(d, cnt, e1);
-        emit_store(d, cnt, e2);
-        emit_store(d, cnt, e3);
+    const uint32_t q = threadIdx.x & 3u;
+    auto span = [&](uint32_t i, uint32_t &off, uint32_t &len) {  // output offset and length of entry i
+        len = 0;
+        off = 16u * i - (tail_rank < i ? 16u - d.tl : 0u);
+        if (i < np && off < rem) len = min(i == tail_rank ? d.tl : 16u, rem - off);
+    };
+    for (uint32_t i0 = threadIdx.x >> 2; i0 < np; i0 += K * LPR) {
+        float4 x[K];
+#pragma unroll
+        for (uint32_t r = 0; r < K; ++r) {
+            uint32_t off, len;
+            const uint32_t i = i0 + r * LPR;
+            span(i, off, len);
+            x[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (vec && len == 16 && (off & 3u) == 0)
+                x[r] = reinterpret_cast<const float4 *>(d.src + (size_t)pos_of(i))[q];
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < K; ++r) {
+            uint32_t off, len;
+            const uint32_t i = i0 + r * LPR;
+            span(i, off, len);
+            if (!len) continue;
+            const uint32_t pos = pos_of(i), o = cnt + off + 4 * q, bi = pos + 4 * q + (uint32_t)d.idx_offset;
+            if (vec && len == 16 && (off & 3u) == 0) {
+                *reinterpret_cast<float4 *>(d.val + o) = x[r];
+                *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+            } else {
+                for (uint32_t c = 0; c < 4; ++c) {
+                    if (4 * q + c < len) {
+                        d.val[o + c] = d.src[(size_t)pos + 4 * q + c];
+                        d.idx[o + c] = bi + c;
+                    }
+                }
+            }
+        }
     }
 }
 
@@ -382,8 +359,14 @@ __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uin
 #ifndef STG_FILL_STAMPS
 #define STG_FILL_STAMPS 0
 #endif
-__global__ void __launch_bounds__(FILL_WG) tv16_fill(Tv16FillArgs A) {
-    __shared__ FillLds S;
+// Registers for 8 waves per SIMD (<= 64 VGPRs): the workgroup's two waves per
+// SIMD run beside the six of two scan workgroups.  The LDS is dynamic: the
+// compiler derives the occupancy it aims for from static LDS and would widen
+// the register budget to the one workgroup per CU that 88 KiB alone allows.
+__global__ void __launch_bounds__(FILL_WG) __attribute__((amdgpu_waves_per_eu(8, 8)))
+tv16_fill(Tv16FillArgs A) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fill_lds[];
+    FillLds &S = *reinterpret_cast<FillLds *>(fill_lds);
     const uint32_t b = blockIdx.x, tid = threadIdx.x;
     uint32_t nst = 0;
     auto stamp = [&](uint32_t v) {
@@ -391,17 +374,36 @@ __global__ void __launch_bounds__(FILL_WG) tv16_fill(Tv16FillArgs A) {
             A.dbg[nst] = v ? v : (uint32_t)__builtin_amdgcn_s_memrealtime();
         ++nst;
     };
+    // which way each regime-B bucket was ordered (debug words 56..59: no
+    // ties, ties by start position, shadow heap, literal heap; tests read them)
+    auto count_path = [&](uint32_t path) {
+        if (tid == 0) atomicAdd(&A.dbg[56 + path], 1u);
+    };
     stamp(0);
     const Tv16FillBucket &d = A.bk[b];
     const Decision &D = A.dec[b];
-    const uint64_t w0 = ld_sc1(&D.w[0]);
+    // the scan launch has finished: every word is final, read them together,
+    // with the first PRE window entries (most buckets have fewer) ahead of
+    // knowing how many there are
+    constexpr uint32_t PRE = 4;
+    const uint32_t *cu = d.cand, *cl = d.cand + CAND_CAP, *ci = d.cand + 2 * CAND_CAP;
+    uint32_t pk[PRE], pl[PRE], pc[PRE];
+#pragma unroll
+    for (uint32_t u = 0; u < PRE; ++u) {
+        const uint32_t e = tid + u * FILL_WG;
+        pk[u] = ld_sc1(&cu[e]);
+        pl[u] = ld_sc1(&cl[e]);
+        pc[u] = ld_sc1(&ci[e]);
+    }
+    static_assert(PRE * FILL_WG <= CAND_CAP, "prefetch inside the window buffer");
+    const uint64_t w0 = ld_sc1(&D.w[0]), w1 = ld_sc1(&D.w[1]), w2 = ld_sc1(&D.w[2]), w3 = ld_sc1(&D.w[3]);
+    const uint32_t failed = ld_sc1(A.fail);
     if ((uint32_t)(w0 >> 32) != ((A.epoch << 8) | TV16_TAG_DEC)) {  // the scan never decided this bucket
         if (tid == 0) { g_or(A.fail, FAIL_SPIN_TIMEOUT); st_sc1(d.count_out, POISON_COUNT); }
         return;
     }
     const uint32_t flags = (uint32_t)w0;
-    if (!(flags & TV16_DEC_B) || ld_sc1(A.fail)) return;  // regime A, or the launch already failed
-    const uint64_t w1 = ld_sc1(&D.w[1]), w2 = ld_sc1(&D.w[2]), w3 = ld_sc1(&D.w[3]);
+    if (!(flags & TV16_DEC_B) || failed) return;  // regime A, or the launch already failed
     const uint32_t cnt = (uint32_t)(w1 >> 32), M = (uint32_t)w1;
     const uint32_t Wtot = (uint32_t)(w2 >> 32);
     const float tail_key = u2f((uint32_t)w2);
@@ -415,219 +417,422 @@ __global__ void __launch_bounds__(FILL_WG) tv16_fill(Tv16FillArgs A) {
     const uint32_t wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
     const bool tail_in = tail && tail_key >= u2f(wlo);
     const uint32_t W = Wtot + (tail_in ? 1u : 0u);
-    bool fast = (flags & TV16_DEC_WIN) && N <= POS_LIM && W <= EMAX && W > 0;
+    bool fast = (flags & TV16_DEC_WIN) && N <= POS_LIM && W <= EMAX && W > 0 && !(A.mode & 2u);
+    uint32_t *const key = S.u.a.key, *const cix = S.u.a.cix;
     // output-order bins over the window below t (sum descending)
     auto obin = [&](uint32_t e) -> uint32_t {
-        const float k = u2f(S.key[e]);
+        const float k = u2f(key[e]);
         if (k >= t) return 0u;
         if (!(k > 0.f)) return NBIN - 1;
-        return min((tb - 1u - S.key[e]) >> 6, NBIN - 1);
+        return min((tb - 1u - key[e]) >> 7, NBIN - 1);
     };
-    auto okey = [&](uint32_t e) -> uint64_t { return (uint64_t)(~ford(u2f(S.key[e]))) << 32; };
-    if (tid == 0) { S.flag = NONE; S.nv = 0; S.maxpos = 0; S.npop = 0; }
-    __syncthreads();
-    if (fast) {
-        const uint32_t *cu = d.cand, *ci = d.cand + 2 * CAND_CAP;
-        for (uint32_t e = tid; e < Wtot; e += FILL_WG) {
-            S.key[e] = ld_sc1(&cu[e]);
-            S.cix[e] = ld_sc1(&ci[e]);
+    auto okey = [&](uint32_t e) -> uint64_t { return (uint64_t)(~ford(u2f(key[e]))) << 32; };
+    auto ksum = [&](uint32_t r) -> float { return u2f(key[S.ord[r]]); };  // sum at rank r
+    auto line_of = [&](uint32_t i) {  // after the node arrays went over S.u.a.line
+        const uint32_t e = S.ord[i];
+        return e == Wtot ? d.nb * 16 : ld_sc1(&d.cand[CAND_CAP + e]);
+    };
+    auto line_lds = [&](uint32_t i) { return S.u.a.line[S.ord[i]]; };
+    // pops needed for the order in S.ord (entries with an output offset < rem) and the tail's rank
+    auto pops = [&](uint32_t &P, uint32_t &tail_rank) {
+        for (uint32_t i = tid; i < W; i += FILL_WG)
+            if (tail_in && S.ord[i] == Wtot) S.flag = i;
+        __syncthreads();
+        tail_rank = S.flag;
+        uint32_t npl = 0;
+        for (uint32_t i = tid; i < W; i += FILL_WG) {
+            const uint32_t off = 16u * i - (tail_rank < i ? 16u - d.tl : 0u);
+            if (off < rem) npl = max(npl, i + 1);
         }
-        if (tail_in && tid == 0) { S.key[Wtot] = f2u(tail_key); S.cix[Wtot] = N - 1; }
+        npl = wave_max(npl);
+        if ((tid & 63u) == 0) atomicMax(&S.npop, npl);
+        __syncthreads();
+        P = S.npop;
+    };
+    if (tid == 0) { S.flag = NONE; S.nv = 0; S.maxpos = 0; S.npop = 0; S.dmax = 0; S.rn = 0; S.nc = 0; S.nu = 0; }
+    __syncthreads();
+    uint32_t P0 = 0, tail_rank0 = NONE;
+    if (fast) {
+#pragma unroll
+        for (uint32_t u = 0; u < PRE; ++u) {
+            const uint32_t e = tid + u * FILL_WG;
+            if (e < Wtot) { key[e] = pk[u]; S.u.a.line[e] = pl[u]; cix[e] = pc[u]; }
+        }
+        for (uint32_t e = tid + PRE * FILL_WG; e < Wtot; e += FILL_WG) {
+            key[e] = ld_sc1(&cu[e]);
+            S.u.a.line[e] = ld_sc1(&cl[e]);
+            cix[e] = ld_sc1(&ci[e]);
+        }
+        if (tail_in && tid == 0) { key[Wtot] = f2u(tail_key); cix[Wtot] = N - 1; S.u.a.line[Wtot] = d.nb * 16; }
         __syncthreads();
         stamp(0);
         // (sum desc, position asc): the output order when no two emitted
         // lines tie; also decides whether the exact heap order is needed
-        counting_sort(S.r.o, S.sh, W, obin, [&](uint32_t e) { return okey(e) | S.cix[e]; });
+        counting_sort(S.u.a.s, S.ord, S.sh, W, obin, [&](uint32_t e) { return okey(e) | cix[e]; });
         stamp(0);
-        // pops needed (entries with an output offset < rem), the tail's rank,
-        // and whether two of the popped lines (or the last popped and the
-        // next) have equal sums
-        uint32_t np_l = 0, tie_l = 0;
-        for (uint32_t i = tid; i < W; i += FILL_WG) {
-            if (tail_in && S.r.o.ord[i] == Wtot) S.flag = i;
-        }
-        __syncthreads();
-        const uint32_t tail_rank0 = S.flag;
-        for (uint32_t i = tid; i < W; i += FILL_WG) {
-            const uint32_t off = 16u * i - (tail_rank0 < i ? 16u - d.tl : 0u);
-            if (off < rem) {
-                np_l = max(np_l, i + 1);
-                if (i + 1 < W && S.key[S.r.o.ord[i]] == S.key[S.r.o.ord[i + 1]]) tie_l = 1;
-            }
-        }
-        np_l = wave_max(np_l);
+        pops(P0, tail_rank0);
+        // two of the popped lines (or the last popped and the next) with equal sums?
+        uint32_t tie_l = 0;
+        for (uint32_t i = tid; i < P0; i += FILL_WG)
+            if (i + 1 < W && ksum(i) == ksum(i + 1)) tie_l = 1;
         tie_l = wave_max(tie_l);
-        if ((tid & 63u) == 0) { atomicMax(&S.npop, np_l); if (tie_l) S.nv = 1; }
+        if ((tid & 63u) == 0 && tie_l) S.nv = 1;
         __syncthreads();
-        const uint32_t P0 = S.npop;
         const bool ties = S.nv != 0;
         const uint32_t covered = 16u * W - (tail_in ? 16u - d.tl : 0u);
         fast = covered >= rem;
         if (fast && !ties) {  // distinct sums: the heap pops them in sum order
-            emit_order(d, cnt, rem, P0, tail_rank0, [&](uint32_t i) {
-                const uint32_t e = S.r.o.ord[i];
-                return e == Wtot ? d.nb * 16 : ld_sc1(&d.cand[CAND_CAP + e]);
-            });
+            emit_order(d, cnt, rem, P0, tail_rank0, line_lds);
+            count_path(0);
             stamp(5);
             return;
         }
-        __syncthreads();
-        if (tid == 0) { S.flag = NONE; S.npop = 0; S.nv = 0; }
-        __syncthreads();
     }
     if (fast) {
-        // ---- the shadow heap (see (1) above) ----
-        // DFS order of the initial positions
-        for (uint32_t e = tid; e < W; e += FILL_WG) S.cix[e] = dkey_of_pos(S.cix[e]);
+        // ---- the shadow heap (see (1) above) over R = ranks [0, rn): every
+        // rank through the first one past the pops, and all that tie with it
+        // (reordering a tie can move the tail, and with it the pop count, by one)
+        const uint32_t pc = min(P0, W - 1);
+        const float kc = ksum(pc);
+        for (uint32_t r = tid; r < W; r += FILL_WG)
+            if (ksum(r) == kc && (r + 1 == W || ksum(r + 1) != kc)) S.rn = r + 1;
         __syncthreads();
-        counting_sort(S.r.a.s, S.sh, W, [&](uint32_t e) { return S.cix[e] >> 14; },
-                      [&](uint32_t e) { return (uint64_t)S.cix[e]; });
+        fast = S.rn < EMAX;  // ranks <= 4094: no content equals CNONE
+    }
+    if (fast) {
+        const uint32_t Rn = S.rn;
+        const uint32_t i0 = PT * tid;  // this thread's ranks, then DFS slots
+        {   // grp: the first rank of each equal-sum run (run starts listed in order)
+            uint32_t stm = 0, nsm = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < PT; ++u) {
+                const uint32_t r = i0 + u;
+                if (r < Rn && (r == 0 || ksum(r - 1) != ksum(r))) { stm |= 1u << u; ++nsm; }
+            }
+            uint32_t tot;
+            const uint32_t so = blk_excl_scan<FNW_F>(nsm, S.sh, &tot);
+            uint16_t *const starts = S.u.a.s.tmp;
+            uint32_t o = so;
+#pragma unroll
+            for (uint32_t u = 0; u < PT; ++u)
+                if (stm >> u & 1u) starts[o++] = (uint16_t)(i0 + u);
+            __syncthreads();
+            uint32_t c = so;
+#pragma unroll
+            for (uint32_t u = 0; u < PT; ++u) {
+                c += stm >> u & 1u;
+                if (i0 + u < Rn) S.grp[i0 + u] = starts[c - 1];
+            }
+            __syncthreads();  // every sum read is done: dk goes over key
+        }
         stamp(0);
-        // nodes: U = the common ancestors of DFS-adjacent elements (pair i owns
-        // those deeper than pair i-1's lowest common ancestor: each node once),
-        // S = each element's start when alone in its subtree: the top of the
-        // largest subtree holding no other element
-        const uint16_t *eo = S.r.a.s.ord;
-        auto L = [&](uint32_t i) -> int { return dk_lca(S.cix[eo[i]], S.cix[eo[i + 1]]); };
-        constexpr uint32_t PT = EMAX / FILL_WG;  // pairs / elements per thread
-        uint32_t nmine = 0;
-        for (uint32_t u = 0; u < PT; ++u) {
-            const uint32_t i = PT * tid + u;
-            if (i + 1 < W) nmine += (uint32_t)max(0, L(i) - (i ? L(i - 1) : -1));
-            if (i < W) {
-                int sh = -1;
-                if (i) sh = max(sh, L(i - 1));
-                if (i + 1 < W) sh = max(sh, L(i));
-                nmine += sh < (int)dk_depth(S.cix[eo[i]]);
+        {   // ---- ties without the heap (see (3) above) ----
+            if (tid == 0) { S.ntl = 0; S.nel = 0; S.flag2 = 0; }
+            __syncthreads();
+            const uint32_t lim = N > P0 + 1 ? N - (P0 + 1) : 0u;
+            for (uint32_t r = tid; r < Rn; r += FILL_WG) {
+                const uint32_t g = S.grp[r];
+                if (g <= P0 && (g != r || (r + 1 < Rn && S.grp[r + 1] == g))) {  // tied, and among the pops
+                    const uint32_t i = atomicAdd(&S.ntl, 1u);
+                    if (i < TCAP) S.tl[i] = (uint16_t)r;
+                }
+                const uint32_t p = cix[S.ord[r]];
+                if (p >= lim) {  // starts among the last P + 1 positions
+                    const uint32_t i = atomicAdd(&S.nel, 1u);
+                    if (i < ECAP) S.el[i] = p;
+                }
+            }
+            __syncthreads();
+            const uint32_t ntl = S.ntl, nel = S.nel;
+            stamp(0);
+            if (STG_FILL_STAMPS && tid == 0 && b == 0) { A.dbg[40] = W; A.dbg[41] = Rn; A.dbg[42] = ntl; A.dbg[43] = nel; A.dbg[44] = P0; }
+            bool bad = ntl > TCAP || nel > ECAP;
+            if (!bad) {
+                for (uint32_t j = tid; j < ntl; j += FILL_WG) {  // a tied line starting above one of its run
+                    const uint32_t tr = S.tl[j], g = S.grp[tr];
+                    const uint32_t qt = cix[S.ord[tr]] + 1, dt = depth_of(qt);
+                    for (uint32_t x = g; x < Rn && S.grp[x] == g; ++x) {
+                        const uint32_t q = cix[S.ord[x]] + 1, dp = depth_of(q);
+                        if (x != tr && dp > dt && (q >> (dp - dt)) == qt) bad = true;
+                    }
+                }
+                if (nel) {  // a line of R at the parent or sibling of a late one
+                    for (uint32_t r = tid; r < Rn; r += FILL_WG) {
+                        const uint32_t p = cix[S.ord[r]];
+                        for (uint32_t j = 0; j < nel; ++j) {
+                            const uint32_t e = S.el[j];
+                            if (e && (p == (e - 1) / 2 || p == (((e - 1) ^ 1u) + 1))) bad = true;
+                        }
+                    }
+                }
+            }
+            if ((__any(bad) || (A.mode & 1u)) && (tid & 63u) == 0) S.flag2 = 1;
+            __syncthreads();
+            stamp(0);
+            if (!S.flag2) {
+                // each run of equal sums in right-first pre-order of its start positions
+                uint16_t *const ord2 = S.u.a.s.tmp;
+                for (uint32_t r = tid; r < Rn; r += FILL_WG) {
+                    const uint32_t g = S.grp[r], kr = rf_key(cix[S.ord[r]]);
+                    uint32_t o = g;
+                    for (uint32_t x = g; x < Rn && S.grp[x] == g; ++x) o += rf_key(cix[S.ord[x]]) < kr;
+                    ord2[o] = S.ord[r];
+                }
+                __syncthreads();
+                for (uint32_t r = tid; r < Rn; r += FILL_WG) S.ord[r] = ord2[r];
+                if (tid == 0) { S.flag = NONE; S.npop = 0; }
+                __syncthreads();
+                uint32_t P, tail_rank;
+                pops(P, tail_rank);
+                stamp(0);
+                emit_order(d, cnt, rem, P, tail_rank, line_lds);
+                count_path(1);
+                stamp(0);
+                stamp(2);
+                return;
             }
         }
+        for (uint32_t r = tid; r < Rn; r += FILL_WG) S.u.b.dk[r] = dkey_of_pos(cix[S.ord[r]]);
+        __syncthreads();  // cix free: eo goes over it
+        // R in DFS order of the start positions
+        counting_sort(S.u.b.s, S.u.b.eo, S.sh, Rn, [&](uint32_t r) { return S.u.b.dk[r] >> 15; },
+                      [&](uint32_t r) { return (uint64_t)S.u.b.dk[r]; });
+        stamp(0);
+        // V in pre-order, built by one scan: DFS slot i emits the ancestors of
+        // its start at depths L(i-1)+1 .. L(i) (L(i): depth of the lowest common
+        // ancestor of slots i and i+1 -- the U nodes, each once), then, when no
+        // other element shares its subtree below max(L(i-1), L(i)), its start
+        // S_i: the ancestor one deeper, where the element sits after its own
+        // subtree's make_heap.  Keys and ranks go to registers first: V is
+        // written over dk / eo.
+        uint32_t kq[PT + 1], rq[PT];
+#pragma unroll
+        for (uint32_t u = 0; u <= PT; ++u) kq[u] = i0 + u < Rn ? S.u.b.dk[S.u.b.eo[i0 + u]] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < PT; ++u) rq[u] = i0 + u < Rn ? S.u.b.eo[i0 + u] : 0u;
+        const uint32_t kp = (i0 >= 1 && i0 - 1 < Rn) ? S.u.b.dk[S.u.b.eo[i0 - 1]] : 0u;
+        auto Lof = [&](uint32_t u) -> int {  // L(i0 + u - 1)
+            const uint32_t i = i0 + u;
+            return (i >= 1 && i < Rn) ? dk_lca(u ? kq[u - 1] : kp, kq[u]) : -1;
+        };
+        uint32_t nmine = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < PT; ++u) {
+            if (i0 + u >= Rn) continue;
+            const int lo = Lof(u), hi = Lof(u + 1);
+            nmine += (uint32_t)max(0, hi - lo) + (max(lo, hi) < (int)dk_depth(kq[u]));
+        }
         uint32_t nv;
-        uint32_t vo = blk_excl_scan<FILL_WG / 64>(nmine, S.sh, &nv);
+        uint32_t vo = blk_excl_scan<FNW_F>(nmine, S.sh, &nv);
         fast = nv <= VCAP;
         if (fast) {
+            uint32_t *const vk = S.u.v.vk;
+            uint2 *const rec = S.u.v.rec;
+#pragma unroll
             for (uint32_t u = 0; u < PT; ++u) {
-                const uint32_t i = PT * tid + u;
-                if (i + 1 < W) {
-                    const int hi = L(i), lo = i ? L(i - 1) : -1;
-                    const uint32_t k = S.cix[eo[i]];
-                    for (int dd = lo + 1; dd <= hi; ++dd) S.r.a.vlist[vo++] = dk_anc(k, (uint32_t)dd);
+                if (i0 + u >= Rn) continue;
+                const int lo = Lof(u), hi = Lof(u + 1);
+                const uint32_t k = kq[u], r = rq[u];
+                const uint32_t ck = ((uint32_t)S.grp[r] << 12) | r;
+                for (int dd = lo + 1; dd <= hi; ++dd, ++vo) {
+                    const uint32_t nk = dk_anc(k, (uint32_t)dd);
+                    vk[vo] = nk;
+                    rec[vo] = r_make(dd == (int)dk_depth(k) ? ck : CNONE, dk_pos(nk), true);
                 }
-            }
-            // starts (held in registers until every thread has read the keys)
-            uint32_t st0 = NONE, st1 = NONE, st2 = NONE, st3 = NONE;
-            static_assert(PT == 4, "four elements per thread");
-            auto start_of = [&](uint32_t i, uint32_t &vo_, uint32_t &st) {
-                if (i >= W) return;
-                int sh = -1;
-                if (i) sh = max(sh, L(i - 1));
-                if (i + 1 < W) sh = max(sh, L(i));
-                const uint32_t k = S.cix[eo[i]];
+                const int sh = max(lo, hi);
                 if (sh < (int)dk_depth(k)) {
-                    st = dk_anc(k, (uint32_t)(sh + 1));
-                    S.r.a.vlist[vo_++] = st;
-                } else {
-                    st = k;  // its own node holds others: a U node
-                }
-            };
-            start_of(PT * tid + 0, vo, st0);
-            start_of(PT * tid + 1, vo, st1);
-            start_of(PT * tid + 2, vo, st2);
-            start_of(PT * tid + 3, vo, st3);
-            __syncthreads();
-            if (st0 != NONE) S.cix[eo[PT * tid + 0]] = st0;
-            if (st1 != NONE) S.cix[eo[PT * tid + 1]] = st1;
-            if (st2 != NONE) S.cix[eo[PT * tid + 2]] = st2;
-            if (st3 != NONE) S.cix[eo[PT * tid + 3]] = st3;
-            __syncthreads();
-            stamp(0);
-            // the nodes in DFS order
-            counting_sort(S.r.a.s, S.sh, nv, [&](uint32_t i) { return S.r.a.vlist[i] >> 14; },
-                          [&](uint32_t i) { return (uint64_t)S.r.a.vlist[i]; });
-            for (uint32_t i = tid; i < nv; i += FILL_WG) S.r.h.vk[i] = S.r.a.vlist[S.r.a.s.ord[i]];
-            __syncthreads();
-            // links and contents
-            for (uint32_t v = tid; v < nv; v += FILL_WG) {
-                S.r.h.vr[v] = (uint16_t)vfind(S, nv, dk_right(S.r.h.vk[v]));
-                S.r.h.vc[v] = NONE16;
-            }
-            __syncthreads();
-            for (uint32_t e = tid; e < W; e += FILL_WG) S.r.h.vc[vfind(S, nv, S.cix[e])] = (uint16_t)e;
-            // internal nodes (a child among the nodes) by depth
-            if (tid <= DMAX + 1) S.uoff[tid] = 0;
-            __syncthreads();
-            for (uint32_t v = tid; v < nv; v += FILL_WG)
-                if (S.r.h.vr[v] != NONE16 || vleft(S, nv, v) != NONE16) atomicAdd(&S.uoff[dk_depth(S.r.h.vk[v]) + 1], 1u);
-            __syncthreads();
-            if (tid == 0) {
-                for (uint32_t dd = 1; dd <= DMAX + 1; ++dd) S.uoff[dd] += S.uoff[dd - 1];
-                for (uint32_t dd = 0; dd <= DMAX; ++dd) S.sh[dd] = S.uoff[dd];
-            }
-            __syncthreads();
-            for (uint32_t v = tid; v < nv; v += FILL_WG)
-                if (S.r.h.vr[v] != NONE16 || vleft(S, nv, v) != NONE16)
-                    S.r.h.ulist[atomicAdd(&S.sh[dk_depth(S.r.h.vk[v])], 1u)] = (uint16_t)v;
-            __syncthreads();
-            stamp(0);
-            // make_heap, deepest level first (a level's subtrees are disjoint)
-            for (int dd = DMAX - 1; dd >= 0; --dd) {
-                const uint32_t o0 = S.uoff[dd], o1 = S.uoff[dd + 1];
-                for (uint32_t i = o0 + tid; i < o1; i += FILL_WG) shadow_sift(S, nv, S.r.h.ulist[i], N);
-                if (o1 > o0) __syncthreads();
-                if (STG_FILL_STAMPS && tid == 0 && b == 0) {
-                    A.dbg[32 + dd] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                    A.dbg[52 + dd / 2] = 0;
+                    const uint32_t nk = dk_anc(k, (uint32_t)(sh + 1));
+                    vk[vo] = nk;
+                    rec[vo] = r_make(ck, dk_pos(nk), false);
+                    ++vo;
                 }
             }
+            if (tid <= NDEP) S.cnt[tid] = 0;
+            if (tid == 0) rec[VCAP] = make_uint2(CNONE, 0u);
+            __syncthreads();
+            // links of the U nodes: the left child follows in pre-order, the
+            // right one is found by binary search (four nodes in lockstep, their
+            // reads in flight together); U nodes per depth; the deepest U depth
+            uint32_t dm = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < NJ; g += 4) {
+                uint32_t lo[4], hi[4], kr[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t v = tid + (g + q) * FILL_WG;
+                    lo[q] = hi[q] = kr[q] = 0;
+                    if (v < nv && r_isu(rec[v])) {
+                        const uint32_t k = vk[v];
+                        kr[q] = dk_right(k);
+                        lo[q] = v + 1;
+                        hi[q] = nv;
+                        dm = max(dm, dk_depth(k) + 1);
+                        atomicAdd(&S.cnt[dk_depth(k)], 1u);
+                    }
+                }
+                if (!__any(kr[0] | kr[1] | kr[2] | kr[3])) continue;  // no U node of this wave here
+                for (uint32_t it = 0; it < 13; ++it) {  // 2^13 > VCAP
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        if (lo[q] < hi[q]) {
+                            const uint32_t m = (lo[q] + hi[q]) >> 1;
+                            if (vk[m] < kr[q]) lo[q] = m + 1; else hi[q] = m;
+                        }
+                    }
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t v = tid + (g + q) * FILL_WG;
+                    if (kr[q]) {
+                        const uint32_t k = vk[v];
+                        const bool hl = v + 1 < nv && vk[v + 1] == dk_left(k);
+                        const bool hr = lo[q] < nv && vk[lo[q]] == kr[q];
+                        rec[v].y |= (hr ? lo[q] << 12 : 0u) | (hl ? 1u << 25 : 0u) | (hr ? 1u << 26 : 0u);
+                    }
+                }
+            }
+            dm = wave_max(dm);
+            if ((tid & 63u) == 0) atomicMax(&S.dmax, dm);
+            __syncthreads();
+            if (tid == 0) {  // U nodes by depth, deepest first
+                uint32_t acc = 0;
+                for (int dd = NDEP - 1; dd >= 0; --dd) { S.uoff[dd] = acc; acc += S.cnt[dd]; }
+                S.nu = acc;
+            }
+            __syncthreads();
+            if (tid < NDEP) S.cnt[tid] = S.uoff[tid];
+            __syncthreads();
+            for (uint32_t j = 0; j < NJ; ++j) {  // over vk: every search is done
+                const uint32_t v = tid + j * FILL_WG;
+                if (v < nv) {
+                    const uint2 rc = rec[v];
+                    if (r_isu(rc)) S.u.w.ul[atomicAdd(&S.cnt[depth_of(r_pos(rc) + 1)], 1u)] = (uint16_t)v;
+                }
+            }
+            __syncthreads();
+            stamp(0);
+            // make_heap on V, top-down and pipelined.  __adjust_heap walks the
+            // larger-child path (right on ties) to the bottom and pushes the
+            // value back up past smaller entries; the path is non-increasing,
+            // so that equals swapping the value down while the larger child is
+            // >= it.  A U node at depth d starts at step Dm - d: its children's
+            // sifts are then one step ahead, their holes two levels below its
+            // own, so every node it reads is final and no two sifts of a step
+            // touch the same node.  Content order: a smaller grp is a larger
+            // sum; CNONE (-inf) has the largest.
+            const uint32_t D1 = S.dmax, nU = S.nu;
             if (STG_FILL_STAMPS && tid == 0 && b == 0) {
-                A.dbg[54] = nv;
-                for (int dd = 0; dd < 8; ++dd) A.dbg[55 + dd] = S.uoff[10 + dd + 1] - S.uoff[10 + dd];
+                A.dbg[40] = W; A.dbg[41] = Rn; A.dbg[42] = nv; A.dbg[43] = D1; A.dbg[44] = P0; A.dbg[46] = nU;
+            }
+            if (D1) {
+                const uint32_t Dm = D1 - 1;
+                uint32_t st[NJ];  // hole | start step << 16 (hole NONE13: done)
+#pragma unroll
+                for (uint32_t j = 0; j < NJ; ++j) {
+                    const uint32_t p = tid + j * FILL_WG;
+                    st[j] = NONE13;
+                    if (p < nU) {
+                        const uint32_t v = S.u.w.ul[p];
+                        st[j] = v | (Dm - depth_of(r_pos(rec[v]) + 1)) << 16;
+                    }
+                }
+                for (uint32_t tau = 0; tau <= 2 * Dm + 1; ++tau) {
+                    // groups of four of this thread's nodes: a group no lane
+                    // of the wave has a live sift in is skipped; otherwise
+                    // every read of the group is issued at once (missing
+                    // nodes read the -inf leaf), then the moves
+#pragma unroll
+                    for (uint32_t g = 0; g < NJ; g += 4) {
+                        bool on[4];
+                        uint32_t hs[4];
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; ++q) {
+                            on[q] = (st[g + q] & NONE13) != NONE13 && (st[g + q] >> 16) <= tau;
+                            hs[q] = on[q] ? (st[g + q] & NONE13) : VCAP;
+                        }
+                        if (!__any(on[0] || on[1] || on[2] || on[3])) continue;
+                        uint2 H[4], La[4], Rb[4];
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; ++q) H[q] = rec[hs[q]];
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; ++q) {
+                            La[q] = rec[r_hasl(H[q]) ? hs[q] + 1 : VCAP];
+                            Rb[q] = rec[r_hasr(H[q]) ? r_right(H[q]) : VCAP];
+                        }
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; ++q) {
+                            if (!on[q]) continue;
+                            const uint32_t h = hs[q], x = r_content(H[q]);
+                            const uint32_t cl = r_content(La[q]), cr = r_content(Rb[q]);
+                            const bool left = (cr >> 12) > (cl >> 12);  // right < left
+                            const uint32_t cm = left ? cl : cr;
+                            if (cm == CNONE || (cm >> 12) > (x >> 12)) {  // the value stays here
+                                st[g + q] = NONE13;
+                            } else {
+                                const uint32_t c = left ? h + 1 : r_right(H[q]);
+                                const uint32_t mx = left ? La[q].x : Rb[q].x;
+                                rec[h].x = cm | (H[q].x & ~CNONE);
+                                rec[c].x = x | (mx & ~CNONE);
+                                st[g + q] = (st[g + q] & ~NONE13) | c;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
             }
             stamp(0);
-            // final positions
-            uint32_t mp = 0;
-            for (uint32_t v = tid; v < nv; v += FILL_WG) {
-                const uint32_t e = S.r.h.vc[v];
-                if (e != NONE16) {
-                    const uint32_t pos = dk_pos(S.r.h.vk[v]);
-                    S.cix[e] = pos;
-                    mp = max(mp, pos);
+            // final positions (by rank, over ul), the deepest one, and a count of R
+            uint32_t mp = 0, nc = 0;
+            for (uint32_t j = 0; j < NJ; ++j) {
+                const uint32_t v = tid + j * FILL_WG;
+                if (v < nv) {
+                    const uint2 rc = rec[v];
+                    const uint32_t c = r_content(rc);
+                    if (c != CNONE) {
+                        const uint32_t pos = r_pos(rc);
+                        S.u.f.fpos[c & 0xfffu] = pos;
+                        mp = max(mp, pos);
+                        ++nc;
+                    }
                 }
             }
             mp = wave_max(mp);
-            if ((tid & 63u) == 0) atomicMax(&S.maxpos, mp);
+            nc = wave_sum(nc);
+            if ((tid & 63u) == 0) { atomicMax(&S.maxpos, mp); atomicAdd(&S.nc, nc); }
             __syncthreads();
-            // output order: sum desc, then right-first pre-order of the position
-            counting_sort(S.r.o, S.sh, W, obin, [&](uint32_t e) { return okey(e) | rf_key(S.cix[e]); });
-            for (uint32_t i = tid; i < W; i += FILL_WG)
-                if (tail_in && S.r.o.ord[i] == Wtot) S.flag = i;
-            __syncthreads();
-            const uint32_t tail_rank = S.flag;
-            uint32_t npl = 0;
-            for (uint32_t i = tid; i < W; i += FILL_WG) {
-                const uint32_t off = 16u * i - (tail_rank < i ? 16u - d.tl : 0u);
-                if (off < rem) npl = max(npl, i + 1);
+            fast = S.nc == Rn;
+        }
+        if (fast) {
+            // equal sums pop in right-first pre-order of their positions (see (2))
+            for (uint32_t r = tid; r < Rn; r += FILL_WG) {
+                const uint32_t g = S.grp[r], kr = rf_key(S.u.f.fpos[r]);
+                uint32_t o = g;
+                for (uint32_t x = g; x < Rn && S.grp[x] == g; ++x) o += rf_key(S.u.f.fpos[x]) < kr;
+                S.u.f.ord2[o] = S.ord[r];
             }
-            npl = wave_max(npl);
-            if ((tid & 63u) == 0) atomicMax(&S.npop, npl);
             __syncthreads();
-            const uint32_t P = S.npop;
+            for (uint32_t r = tid; r < Rn; r += FILL_WG) S.ord[r] = S.u.f.ord2[r];
+            if (tid == 0) { S.flag = NONE; S.npop = 0; }
+            __syncthreads();
+            uint32_t P, tail_rank;
+            pops(P, tail_rank);
             stamp(0);
+            if (STG_FILL_STAMPS && tid == 0 && b == 0) A.dbg[45] = P;
             // the pops never reinsert an element of R (see (2) above)
-            if (S.maxpos + P < N) {
-                emit_order(d, cnt, rem, P, tail_rank, [&](uint32_t i) {
-                    const uint32_t e = S.r.o.ord[i];
-                    return e == Wtot ? d.nb * 16 : ld_sc1(&d.cand[CAND_CAP + e]);
-                });
+            if (S.maxpos + P < N && P <= Rn) {
+                emit_order(d, cnt, rem, P, tail_rank, line_of);
+                count_path(2);
                 stamp(1);
                 return;
             }
             fast = false;
         }
-        __syncthreads();
-        if (tid == 0) { S.flag = NONE; S.npop = 0; }
-        __syncthreads();
     }
+    __syncthreads();
+    if (tid == 0) { S.flag = NONE; S.npop = 0; }
+    __syncthreads();
     stamp(3);
+    count_path(3);
     full_path(S, d, cnt, N, t, tail, tail_key, A.fail);
     stamp(0);
 }
@@ -636,7 +841,11 @@ __global__ void __launch_bounds__(FILL_WG) tv16_fill(Tv16FillArgs A) {
 
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {
     if (!a.nbk) return hipSuccess;
-    tv16_fill<<<a.nbk, FILL_WG, 0, s>>>(a);
+    static const hipError_t attr =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&tv16_fill), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(FillLds));
+    if (attr != hipSuccess) return attr;
+    tv16_fill<<<a.nbk, FILL_WG, sizeof(FillLds), s>>>(a);
     return hipGetLastError();
 }
 

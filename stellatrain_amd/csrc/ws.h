@@ -11,6 +11,7 @@ namespace stg {
 constexpr uint32_t CAND_CAP = 4096;          // regime-B window entries per bucket (+1 for the ragged tail)
 constexpr uint32_t CAND_WORDS = 4 * CAND_CAP; // per bucket: line-sum bits | line position | candidate index | spare
 constexpr uint32_t TV16_WIN = 1u << 17;      // regime-B window below t, in ulps of t (~1.6 %)
+constexpr uint32_t TV16_SCAN_LDS = 35584;     // LDS bytes of a scan workgroup (bound; tv16.hip checks)
 
 constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)
 constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
@@ -107,6 +108,7 @@ struct Tv16Launch {
     uint32_t epoch;    // per-workspace call counter, 1..2^24-1 (hand-off tags)
     uint32_t max_wg;     // fused-kernel workgroups at most (its share of 2 per CU)
     uint32_t desc_cap;   // ChunkDesc entries at ws.desc
+    hipEvent_t scan_done;  // optional: recorded between the scan and the fill launch
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
 // thresholdv16 regime-B heap fill (tv16fill.hip): one workgroup per bucket
@@ -127,6 +129,7 @@ struct Tv16FillArgs {
     const Decision *dec;
     uint32_t *fail;
     uint32_t *dbg;         // diagnostics: phase stamps of workgroup 0 (ws.misc)
+    uint32_t mode;         // tests (STG_DEBUG_TV16_FILL): 1 = always the shadow heap, 2 = always the literal heap
 };
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
 

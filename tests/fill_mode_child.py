@@ -1,0 +1,58 @@
+"""Child process of tests/test_gpu_fill_modes.py (not a test module).
+
+Runs thresholdv16 AIMD sequences whose regime-B calls tie inside the heap
+fill, with STG_DEBUG_TV16_FILL set by the parent (read once per process:
+0 = production, 1 = always the shadow heap, 2 = always the literal heap),
+checks every call's whole stream against the oracle, and prints the fill's
+path counters (debug words 56..59) as one JSON line.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    import torch
+    from oracle.oracle import Oracle
+    from parity import assert_same_stream
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel
+    from stellatrain_amd._capi import check, lib
+    from stellatrain_amd.synth import D1, seed_for, synth
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    o = Oracle()
+    ho = o.tv16_new()
+    comp = ThresholdvCompressor16()
+    cases = [(1 << 20, 10485, 6), (4 << 20, 41943, 5), (16 << 20, 167772, 4)]
+    if os.environ.get("STG_DEBUG_TV16_FILL") == "2":
+        cases = cases[:2]  # the literal heap takes milliseconds per call at 64 MiB
+    calls = 0
+    for ci, (n, k, iters) in enumerate(cases):
+        key = f"fm{ci}"
+        idx = torch.zeros(k, dtype=torch.int32, device=dev)
+        val = torch.zeros(k, dtype=torch.float32, device=dev)
+        for it in range(iters):
+            x = synth(n, seed_for(700 + ci, it), D1)
+            cnt = comp.compress(key, torch.from_numpy(x).to(dev), k, idx, val)
+            co, io, vo = o.tv16_compress(ho, key, x, k)
+            assert cnt == co, (n, it)
+            assert_same_stream(idx.cpu().numpy().view(np.uint32), val.cpu().numpy(), io, vo, co)
+            calls += 1
+    comp.check_device()
+    w = (C.c_uint32 * 64)()
+    check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
+    print(json.dumps({"ok": True, "calls": calls, "paths": list(w)[56:60],
+                      "mode": os.environ.get("STG_DEBUG_TV16_FILL")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

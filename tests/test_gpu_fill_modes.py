@@ -1,0 +1,48 @@
+"""Every way the regime-B heap fill orders equal sums gives the reference's stream.
+
+tv16fill.hip orders a regime-B bucket's heap pops one of four ways: no two
+popped sums tie (sum order), ties ordered by right-first pre-order of their
+start positions (when its two checks pass), the shadow heap, or the literal
+make_heap / pop_heap in global memory.  STG_DEBUG_TV16_FILL forces the
+heavier ways, so each is checked against the oracle on the same tie-heavy
+AIMD sequences; the fill's path counters show which way ran.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _child(mode: int):
+    env = dict(os.environ, STG_DEBUG_TV16_FILL=str(mode))
+    r = subprocess.run([sys.executable, os.path.join(HERE, "fill_mode_child.py")],
+                       capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_production_order(gpu):
+    out = _child(0)
+    none, by_start, shadow, literal = out["paths"]
+    assert by_start > 0, out  # D1's regime-B calls tie among the pops
+    assert literal == 0, out
+
+
+def test_shadow_heap_order(gpu):
+    out = _child(1)
+    none, by_start, shadow, literal = out["paths"]
+    assert by_start == 0 and shadow > 0 and literal == 0, out
+
+
+def test_literal_heap_order(gpu):
+    out = _child(2)
+    none, by_start, shadow, literal = out["paths"]
+    assert by_start == 0 and shadow == 0 and literal > 0, out

@@ -23,23 +23,22 @@ def main():
     n = 16 << 20
     k = merge_numel(n, 0.99)
     comp = ThresholdvCompressor16()
-    bufs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(8)]
+    nbk = int(os.environ.get("FS_BUCKETS", "8"))
+    bufs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in range(nbk)]
     outs = [(torch.zeros(k, dtype=torch.int32, device=dev), torch.zeros(k, dtype=torch.float32, device=dev))
-            for _ in range(8)]
+            for _ in range(nbk)]
     for it in range(10):
         for i, b in enumerate(bufs):
-            check(lib().stg_synth_fill_device(C.c_void_p(b.data_ptr()), n, seed_for(i, it), 0, 0,
+            check(lib().stg_synth_fill_device(C.c_void_p(b.data_ptr()), n, seed_for(i, it % 2 if os.environ.get("FS_PARITY") else it), 0, 0,
                                               C.c_void_p(st.cuda_stream)))
-        comp.compress_batch_async([(f"{i}@w", bufs[i], k, outs[i][0], outs[i][1]) for i in range(8)])
+        comp.compress_batch_async([(f"{i}@w", bufs[i], k, outs[i][0], outs[i][1]) for i in range(nbk)])
         w = (C.c_uint32 * 64)()
         check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
         v = list(w)
         print(json.dumps({"it": it, "raw": v[:14]}), flush=True)
         ts = [x for x in v[:16] if x > 1000]
         marks = [x for x in v[:16] if 0 < x <= 1000]
-        lv = [v[32 + dd] for dd in range(19, -1, -1)]
-        print(json.dumps({"it": it, "level_us": [round((lv[j + 1] - lv[j]) / 100.0, 2) for j in range(len(lv) - 1)],
-                          "nv": v[54], "counts10_17": v[55:63]}), flush=True)
+        print(json.dumps({"it": it, "W_Rn_nv_D1_P0_P_nU": v[40:47], "paths": v[56:60]}), flush=True)
         print(json.dumps({"it": it, "phase_us": [round((ts[j + 1] - ts[j]) / 100.0, 2) for j in range(len(ts) - 1)],
                           "marks": marks}), flush=True)
         for j in range(64):

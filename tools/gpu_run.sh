@@ -26,7 +26,7 @@ for s in "$@"; do
     case $s in
         tests) step tests 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
         tests_all) step tests_all 900 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
-        tests_tv16) step tests_tv16 600 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_coresidency.py -v -m gpu --timeout 120 --timeout-method thread ;;
+        tests_tv16) step tests_tv16 600 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_coresidency.py tests/test_gpu_fill_modes.py -v -m gpu --timeout 120 --timeout-method thread ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
         bench) step bench 400 python bench.py ;;
         bench_short) step bench_short 300 python bench.py --steps 40 --warmup 8 --cpu-seconds 5 ;;
