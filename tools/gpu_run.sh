@@ -38,7 +38,7 @@ for s in "$@"; do
                 -d "$R/gpurun_out/pmc_fetch" -o run -- python3 bench.py --steps 16 --warmup 4 --profile-steps 4 --no-cpu-baseline ;;
         pmc_write) step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
                 -d "$R/gpurun_out/pmc_write" -o run -- python3 bench.py --steps 16 --warmup 4 --profile-steps 4 --no-cpu-baseline ;;
-        prof_s1|prof_s2|prof_s3|prof_s5)
+        prof_s1|prof_s3)  # scan work only (1) / plain streaming read (3): STG_DEBUG_TV16_STAGE
             export STG_DEBUG_TV16_STAGE=${s#prof_s}
             step $s 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$s" -o run \
                 -- python3 bench.py --steps 50 --warmup 8 --no-cpu-baseline
@@ -68,13 +68,13 @@ for s in "$@"; do
                 fi
                 unset STG_CODEC_LIB
             done ;;
-        sweep)
-            for W in 1 2; do for S in 1 2; do for K in 8 16; do
-                export STG_TV16_WGPERCU=$W
-                step sweep_w${W}_s${S}_k${K} 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline --streams $S --keys $K
-            done; done; done
-            unset STG_TV16_WGPERCU ;;
-        stamps) export STG_DEBUG_TV16_STAGE=4; step stamps 300 python tools/stamps.py; unset STG_DEBUG_TV16_STAGE ;;
+        streams)  # headline stream counts, default admission vs scans one at a time
+            for S in 1 2 3 4; do
+                step streams_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
+                STG_TV16_SERIAL=1 step streams_serial_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
+            done ;;
+        fill_stamps) FS_BUCKETS=16 FS_PARITY=1 STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so \
+                step fill_stamps 200 python tools/fill_stamps.py ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
     esac
 done
