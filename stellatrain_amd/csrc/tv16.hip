@@ -182,7 +182,7 @@ static_assert(sizeof(Lds) <= TV16_SCAN_LDS, "two scan workgroups and a fill work
 
 // Spin-timeout failure bits: FAIL_SPIN_TIMEOUT plus bit 8 + site naming the
 // wait that gave up: 1 buffer set, 2 prefix aggregates, 3 chunk streamed,
-// 6 / 7 slot chunk id (streamer / finisher), 8 the previous slot's chunk take.
+// 6 / 7 slot chunk id (streamer / finisher).
 __device__ __forceinline__ constexpr uint32_t spin_site(uint32_t site) { return FAIL_SPIN_TIMEOUT | (1u << (8 + site)); }
 
 struct Ctx {
@@ -293,15 +293,14 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
     float4 v[SCAN_D];
 #pragma unroll
     for (uint32_t u = 0; u < SCAN_D; ++u) v[u] = load(u);
-    // The first wave past the middle of slot j takes the chunk of slot j + 2
-    // from the call's counter (slots 0 and 1 at the start): late enough that
-    // chunks are taken close to when they are streamed (the finishers' prefix
-    // counts wait on earlier chunks only), early enough that the round trip
-    // hides behind the second half of the slot.  A take waits until slot
-    // j - 1's take is published (slot j + 1's chunk id), so a workgroup's
-    // chunk ids increase slot by slot and the first id >= K ends it with no
-    // chunk left behind -- a wave with no steps in a short chunk could
-    // otherwise run ahead into slot j + 1 and take before slot j did.
+    // The first wave past the middle of slot j takes the chunk of slot j + 1
+    // from the call's counter (slot 0 at the start): late enough that chunks
+    // are taken close to when they are streamed (the finishers' prefix counts
+    // wait on earlier chunks only) and that a short batch spreads one chunk
+    // per workgroup, early enough that the round trip hides behind the second
+    // half of the slot.  Every wave in slot j has seen slot j's chunk id, so a
+    // workgroup's chunk ids increase slot by slot and the first id >= K ends
+    // it with no chunk left behind.
     uint32_t nx = 0;
     bool grab = false, tried = false;
     auto try_take = [&]() {
@@ -311,9 +310,8 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
         grab = uni(first) == 0;
         if (grab && flane() == 0) nx = g_add(&C.cc()->next, 1u);
     };
-    auto prev_taken = [&]() { return lds_ld(&L.cok[(j + 1) % CIDR]) == j + 2; };
     for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
-        if (!tried && m0 >= mine / 2 && prev_taken()) try_take();
+        if (!tried && m0 >= mine / 2) try_take();
 #pragma unroll
         for (uint32_t u = 0; u < SCAN_D; ++u) {
             const float4 x = v[u];
@@ -368,21 +366,14 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
             }
         }
     }
-    if (!tried) {  // no steps here (a short chunk) or slot j - 1's take came late
-        uint64_t st3 = 0;
-        for (uint32_t spins = 0; !prev_taken(); ++spins) {
-            __builtin_amdgcn_s_sleep(1);
-            if (spin_expired(spins, st3)) { if (flane() == 0) C.spin_fail(8, j, lds_ld(&L.cok[(j + 1) % CIDR]), s); break; }
-        }
-        try_take();
-    }
+    if (!tried) try_take();  // no steps here (a short chunk)
     if (grab && flane() == 0) {
         // slot j + NBUF reuses slot j - NBUF's counter: every wave is done
         // with slot j - NBUF (the finisher released it) and none is past j yet
         L.mid[(j + NBUF) % CIDR] = 0;
-        L.cid[(j + 2) % CIDR] = nx;
+        L.cid[(j + 1) % CIDR] = nx;
         lds_drain();
-        lds_st(&L.cok[(j + 2) % CIDR], j + 3);
+        lds_st(&L.cok[(j + 1) % CIDR], j + 2);
     }
     if (lane == 0) {
         if (cnt_w) atomicAdd(&L.qcnt[par], cnt_w);
@@ -678,17 +669,14 @@ tv16_batch(BatchArgs A) {
     }
     if (threadIdx.x == 0) {
         L.fdone = 0;
-        // slots 0 and 1: the next two chunks of the call's counter, taken as
-        // the workgroup starts; later slots take one each mid-slot.  A
+        // slot 0: the next chunk of the call's counter, taken as the
+        // workgroup starts; later slots take one each mid-slot.  A
         // workgroup's slots therefore hold increasing chunks, chunks are taken
         // in order, and a chunk is only ever taken by a running workgroup: no
         // wait in this launch points at a workgroup that is not resident.
-        const uint32_t c0 = g_add(&C.cc()->next, 2u);
-        L.cid[0] = c0;
-        L.cid[1] = c0 + 1;
+        L.cid[0] = g_add(&C.cc()->next, 1u);
         for (uint32_t i = 0; i < CIDR; ++i) { L.cok[i] = 0; L.mid[i] = 0; }
         L.cok[0] = 1;
-        L.cok[1] = 2;
     }
     __syncthreads();
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

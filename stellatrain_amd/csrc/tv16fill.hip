@@ -59,7 +59,7 @@ using namespace tv16;
 
 constexpr uint32_t FILL_WG = 512;              // 8 waves: beside two 12-wave scan workgroups
 constexpr uint32_t FNW_F = FILL_WG / 64;
-constexpr uint32_t EMAX = CAND_CAP;            // window entries + the ragged tail
+constexpr uint32_t EMAX = 4096;                // window entries kept (+ the ragged tail)
 constexpr uint32_t VCAP = 6144;                // shadow-heap nodes held (more: full path)
 constexpr uint32_t POS_LIM = (1u << 20) - 1;   // fast path: N <= POS_LIM (20-bit paths)
 constexpr uint32_t NONE = 0xffffffffu;
@@ -72,7 +72,7 @@ constexpr uint32_t NJ = VCAP / FILL_WG;        // nodes per thread
 constexpr uint32_t TCAP = 256;                 // tied ranks checked without the heap (more: the heap)
 constexpr uint32_t ECAP = 64;                  // late start positions checked (more: the heap)
 static_assert(VCAP < NONE13, "13-bit node indices");
-static_assert(NBIN << 7 == TV16_WIN, "output-sort bins of 128 ulps cover the window");
+static_assert(NBIN << 8 == TV16_WIN, "output-sort bins of 256 ulps cover the window");
 
 // A heap node as a DFS key: its path from the root left-aligned to depth 19
 // (20 bits) << 5 | its depth.  Ascending keys = pre-order, left subtree first;
@@ -157,7 +157,7 @@ struct FillLds {
     uint32_t cnt[NDEP + 1], uoff[NDEP + 1];
     uint16_t tl[TCAP];  // tied ranks among the pops
     uint32_t el[ECAP];  // start positions of R among the last P + 1
-    uint32_t flag, nv, maxpos, npop, dmax, rn, nc, nu, ntl, nel, flag2;
+    uint32_t flag, nv, maxpos, npop, dmax, rn, nc, nu, ntl, nel, flag2, et;
 };
 static_assert(sizeof(FillLds) + 2 * TV16_SCAN_LDS <= 160 * 1024, "a fill workgroup beside two scan workgroups");
 static_assert(EMAX <= 4096, "ranks fit the 12-bit content fields");
@@ -385,15 +385,17 @@ tv16_fill(Tv16FillArgs A) {
     // the scan launch has finished: every word is final, read them together,
     // with the first PRE window entries (most buckets have fewer) ahead of
     // knowing how many there are
-    constexpr uint32_t PRE = 4;
+    constexpr uint32_t PRE = 8, PREX = 8;  // keys / lines and indices prefetched per thread
     const uint32_t *cu = d.cand, *cl = d.cand + CAND_CAP, *ci = d.cand + 2 * CAND_CAP;
-    uint32_t pk[PRE], pl[PRE], pc[PRE];
+    uint32_t pk[PRE], pl[PREX], pc[PREX];
 #pragma unroll
     for (uint32_t u = 0; u < PRE; ++u) {
         const uint32_t e = tid + u * FILL_WG;
         pk[u] = ld_sc1(&cu[e]);
-        pl[u] = ld_sc1(&cl[e]);
-        pc[u] = ld_sc1(&ci[e]);
+        if (u < PREX) {
+            pl[u] = ld_sc1(&cl[e]);
+            pc[u] = ld_sc1(&ci[e]);
+        }
     }
     static_assert(PRE * FILL_WG <= CAND_CAP, "prefetch inside the window buffer");
     const uint64_t w0 = ld_sc1(&D.w[0]), w1 = ld_sc1(&D.w[1]), w2 = ld_sc1(&D.w[2]), w3 = ld_sc1(&D.w[3]);
@@ -416,27 +418,30 @@ tv16_fill(Tv16FillArgs A) {
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
     const bool tail_in = tail && tail_key >= u2f(wlo);
-    const uint32_t W = Wtot + (tail_in ? 1u : 0u);
-    bool fast = (flags & TV16_DEC_WIN) && N <= POS_LIM && W <= EMAX && W > 0 && !(A.mode & 2u);
+    bool fast = (flags & TV16_DEC_WIN) && N <= POS_LIM && Wtot + (tail_in ? 1u : 0u) > 0 && !(A.mode & 2u);
+    if (!fast && tid == 0) {  // why the literal heap (debug words 60..63)
+        if (!(flags & TV16_DEC_WIN)) atomicAdd(&A.dbg[60], 1u);
+        if (N > POS_LIM) atomicAdd(&A.dbg[61], 1u);
+    }
     uint32_t *const key = S.u.a.key, *const cix = S.u.a.cix;
     // output-order bins over the window below t (sum descending)
-    auto obin = [&](uint32_t e) -> uint32_t {
-        const float k = u2f(key[e]);
+    auto kbin = [&](uint32_t kb) -> uint32_t {
+        const float k = u2f(kb);
         if (k >= t) return 0u;
         if (!(k > 0.f)) return NBIN - 1;
-        return min((tb - 1u - key[e]) >> 7, NBIN - 1);
+        return min((tb - 1u - kb) >> 8, NBIN - 1);
     };
+    auto obin = [&](uint32_t e) -> uint32_t { return kbin(key[e]); };
     auto okey = [&](uint32_t e) -> uint64_t { return (uint64_t)(~ford(u2f(key[e]))) << 32; };
     auto ksum = [&](uint32_t r) -> float { return u2f(key[S.ord[r]]); };  // sum at rank r
-    auto line_of = [&](uint32_t i) {  // after the node arrays went over S.u.a.line
-        const uint32_t e = S.ord[i];
-        return e == Wtot ? d.nb * 16 : ld_sc1(&d.cand[CAND_CAP + e]);
-    };
+    uint32_t W = 0, Et = NONE;  // entries kept, the ragged tail's element id
+    uint32_t *const lines_g = reinterpret_cast<uint32_t *>(d.heap);  // element -> line, for the shadow path
+    auto line_of = [&](uint32_t i) { return ld_sc1(&lines_g[S.ord[i]]); };  // after V went over S.u.a.line
     auto line_lds = [&](uint32_t i) { return S.u.a.line[S.ord[i]]; };
     // pops needed for the order in S.ord (entries with an output offset < rem) and the tail's rank
     auto pops = [&](uint32_t &P, uint32_t &tail_rank) {
         for (uint32_t i = tid; i < W; i += FILL_WG)
-            if (tail_in && S.ord[i] == Wtot) S.flag = i;
+            if (S.ord[i] == Et) S.flag = i;
         __syncthreads();
         tail_rank = S.flag;
         uint32_t npl = 0;
@@ -449,26 +454,81 @@ tv16_fill(Tv16FillArgs A) {
         __syncthreads();
         P = S.npop;
     };
-    if (tid == 0) { S.flag = NONE; S.nv = 0; S.maxpos = 0; S.npop = 0; S.dmax = 0; S.rn = 0; S.nc = 0; S.nu = 0; }
+    if (tid == 0) { S.flag = NONE; S.nv = 0; S.maxpos = 0; S.npop = 0; S.dmax = 0; S.rn = 0; S.nc = 0; S.nu = 0; S.et = NONE; }
     __syncthreads();
     uint32_t P0 = 0, tail_rank0 = NONE;
     if (fast) {
+        // ---- the output order of the top of the window, in one counting
+        // sort: bins of 256 ulps below t (sum descending), cut after the first
+        // bins that hold M + 2 entries (every pop, the first entry past them
+        // and its ties: a bin never splits equal sums), at most EMAX; the
+        // window lists up to CAND_CAP.  An entry's id is its slot in the
+        // bin-grouped arrays; inside a bin, (sum desc, position asc). ----
+        SortScratch &X = S.u.a.s;
+        stamp(0);
+        for (uint32_t i = tid; i < NBIN; i += FILL_WG) X.bin[i] = 0;
+        __syncthreads();
 #pragma unroll
-        for (uint32_t u = 0; u < PRE; ++u) {
-            const uint32_t e = tid + u * FILL_WG;
-            if (e < Wtot) { key[e] = pk[u]; S.u.a.line[e] = pl[u]; cix[e] = pc[u]; }
-        }
-        for (uint32_t e = tid + PRE * FILL_WG; e < Wtot; e += FILL_WG) {
-            key[e] = ld_sc1(&cu[e]);
-            S.u.a.line[e] = ld_sc1(&cl[e]);
-            cix[e] = ld_sc1(&ci[e]);
-        }
-        if (tail_in && tid == 0) { key[Wtot] = f2u(tail_key); cix[Wtot] = N - 1; S.u.a.line[Wtot] = d.nb * 16; }
+        for (uint32_t u = 0; u < PRE; ++u)
+            if (tid + u * FILL_WG < Wtot) atomicAdd(&X.bin[kbin(pk[u])], 1u);
+        for (uint32_t e = tid + PRE * FILL_WG; e < Wtot; e += FILL_WG) atomicAdd(&X.bin[kbin(ld_sc1(&cu[e]))], 1u);
+        if (tail_in && tid == 0) atomicAdd(&X.bin[kbin(f2u(tail_key))], 1u);
         __syncthreads();
         stamp(0);
-        // (sum desc, position asc): the output order when no two emitted
-        // lines tie; also decides whether the exact heap order is needed
-        counting_sort(S.u.a.s, S.ord, S.sh, W, obin, [&](uint32_t e) { return okey(e) | cix[e]; });
+        {
+            constexpr uint32_t PER = NBIN / FILL_WG;
+            static_assert(PER == 2, "two bins per thread");
+            const uint32_t c0 = X.bin[PER * tid], c1 = X.bin[PER * tid + 1], need = M + 2;
+            uint32_t tot;
+            const uint32_t run = blk_excl_scan<FNW_F>(c0 + c1, S.sh, &tot);
+            X.bin[PER * tid] = X.cur[PER * tid] = run;
+            X.bin[PER * tid + 1] = X.cur[PER * tid + 1] = run + c0;
+            if (run < need && run + c0 >= need) { S.flag = PER * tid + 1; S.nv = run + c0; }
+            else if (run + c0 < need && run + c0 + c1 >= need) { S.flag = PER * tid + 2; S.nv = run + c0 + c1; }
+            if (tid == 0 && tot < need) { S.flag = NBIN; S.nv = tot; }
+            __syncthreads();
+        }
+        const uint32_t cut = S.flag;  // bins [0, cut) are kept
+        W = S.nv;
+        fast = W <= EMAX;
+        if (!fast && tid == 0) atomicAdd(&A.dbg[62], 1u);
+        if (fast) {
+            auto keep = [&](uint32_t kb, uint32_t line, uint32_t cx, bool is_tail) {
+                const uint32_t e = atomicAdd(&X.cur[kbin(kb)], 1u);
+                key[e] = kb;
+                S.u.a.line[e] = line;
+                cix[e] = cx;
+                st_sc1(&lines_g[e], line);
+                if (is_tail) S.et = e;
+            };
+#pragma unroll
+            for (uint32_t u = 0; u < PRE; ++u) {
+                const uint32_t e = tid + u * FILL_WG;
+                if (e >= Wtot || kbin(pk[u]) >= cut) continue;
+                if (u < PREX) keep(pk[u], pl[u], pc[u], false);
+                else keep(pk[u], ld_sc1(&cl[e]), ld_sc1(&ci[e]), false);
+            }
+            for (uint32_t e = tid + PRE * FILL_WG; e < Wtot; e += FILL_WG) {
+                const uint32_t kb = ld_sc1(&cu[e]);
+                if (kbin(kb) < cut) keep(kb, ld_sc1(&cl[e]), ld_sc1(&ci[e]), false);
+            }
+            if (tail_in && tid == 0 && kbin(f2u(tail_key)) < cut) keep(f2u(tail_key), d.nb * 16, N - 1, true);
+            __syncthreads();
+            stamp(0);
+            for (uint32_t e = tid; e < W; e += FILL_WG) {
+                const uint32_t bb = kbin(key[e]), lo = X.bin[bb], hi = X.cur[bb];
+                const uint64_t k = okey(e) | cix[e];
+                uint32_t r = lo;
+                for (uint32_t x = lo; x < hi; ++x) r += (okey(x) | cix[x]) < k;
+                S.ord[r] = (uint16_t)e;
+            }
+        }
+        Et = S.et;
+        __syncthreads();
+        if (tid == 0) { S.flag = NONE; S.nv = 0; }
+        __syncthreads();
+    }
+    if (fast) {
         stamp(0);
         pops(P0, tail_rank0);
         // two of the popped lines (or the last popped and the next) with equal sums?
@@ -479,8 +539,9 @@ tv16_fill(Tv16FillArgs A) {
         if ((tid & 63u) == 0 && tie_l) S.nv = 1;
         __syncthreads();
         const bool ties = S.nv != 0;
-        const uint32_t covered = 16u * W - (tail_in ? 16u - d.tl : 0u);
+        const uint32_t covered = 16u * W - (Et != NONE ? 16u - d.tl : 0u);
         fast = covered >= rem;
+        if (!fast && tid == 0) atomicAdd(&A.dbg[63], 1u);
         if (fast && !ties) {  // distinct sums: the heap pops them in sum order
             emit_order(d, cnt, rem, P0, tail_rank0, line_lds);
             count_path(0);

@@ -8,9 +8,9 @@
 
 namespace stg {
 
-constexpr uint32_t CAND_CAP = 4096;          // regime-B window entries per bucket (+1 for the ragged tail)
+constexpr uint32_t CAND_CAP = 8192;          // regime-B window entries per bucket (+1 for the ragged tail)
 constexpr uint32_t CAND_WORDS = 4 * CAND_CAP; // per bucket: line-sum bits | line position | candidate index | spare
-constexpr uint32_t TV16_WIN = 1u << 17;      // regime-B window below t, in ulps of t (~1.6 %)
+constexpr uint32_t TV16_WIN = 1u << 18;      // regime-B window below t, in ulps of t (~3.1 %)
 constexpr uint32_t TV16_SCAN_LDS = 35584;     // LDS bytes of a scan workgroup (bound; tv16.hip checks)
 
 constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)

@@ -426,9 +426,10 @@ def gather(torch, calls):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
-    p.add_argument("--c4-streams", type=int, default=1)
-    p.add_argument("--only", default="c2,c3,c4,c5,e2e,apply,ef,gather")
+    p.add_argument("--c4-streams", type=int, default=4)
+    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,ef,gather")
     a = p.parse_args()
+    os.environ.setdefault("STG_TV16_INFLIGHT", str(min(4, a.c4_streams)))
     import torch
     from stellatrain_amd import make_compressor
     only = set(a.only.split(","))
@@ -442,6 +443,8 @@ def main():
         emit(host_inclusive(torch, "thresholdv16", 64, 0.99, 24))
     if "c4" in only:
         emit(c4_stream(torch, 3, a.c4_streams))
+    if "single" in only:  # one 64 MiB bucket per call, one stream: the latency of a lone call
+        emit(time_device(torch, make_compressor("thresholdv16"), "thresholdv16 single-bucket", 64, 0.99, a.calls, 8, 16))
     if "c5" in only:
         for kind in ("sgd", "adam", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))

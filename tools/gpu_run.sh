@@ -45,6 +45,7 @@ for s in "$@"; do
             unset STG_DEBUG_TV16_STAGE ;;
         ubench) step ubench 300 python tools/ubench_read.py ;;
         configs) step configs 500 python tools/bench_configs.py ;;
+        single) step single 200 python tools/bench_configs.py --only single ;;
         c2) step c2 300 python tools/bench_configs.py --only c2 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
