@@ -487,7 +487,9 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         HIP_TRY(stg::launch_tv(a, ws->d, s));
     } else {
         const size_t ntiles = (n + stg::TV_TILE - 1) / stg::TV_TILE;
-        if ((rc = ws->ensure(1, 2 * ntiles + 1, 1))) return rc;  // per-tile counts, then their prefix
+        // superset entries (two words each, stg::TOPK_SUP_CAP per tile); per-tile
+        // counts, their prefixes and the superset counts
+        if ((rc = ws->ensure(2 * ntiles * stg::TOPK_SUP_CAP, 3 * ntiles + 1, 1))) return rc;
         stg::TopkLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, h->method == M_TOPK, d_count,
                           h->num_cu, ev};
         HIP_TRY(stg::launch_topk(a, ws->d, s));

@@ -12,7 +12,7 @@
 // cluster in a few exponents -- rarely hit one LDS address together) and one
 // global atomic per non-empty bin; then one 1024-thread workgroup picks the
 // bin holding the rank and zeroes the table.
-#include "ws.h"
+#include "select.h"
 
 namespace stg {
 
@@ -26,68 +26,10 @@ namespace {
 #endif
 constexpr uint32_t NCOPY = STG_RS_NCOPY;
 constexpr uint32_t HWG = 1024;  // rs_hist workgroup: one fat workgroup per CU, few global bin atomics
-constexpr uint32_t PWG = 1024;  // rs_pick workgroup: two bins per thread at 11 bits
-
-// The bin holding the rank, counting from the top bin, by one 1024-thread
-// workgroup: each thread sums its (top-down) bins, a workgroup scan finds the
-// thread whose range holds the rank, that thread walks its bins.  It also
-// zeroes the histogram for the next level (and the next select: the table is
-// zero at allocation and after every complete select, so no init launch).
-// The first level (SHIFT + NBITS == 31) takes the rank from the arguments and
-// starts the prefix afresh.
-template <int SHIFT, int NBITS>
-__global__ void __launch_bounds__(PWG) rs_pick(RSel *st, uint64_t extra_zeros, const uint32_t *d_rank,
-                                              uint32_t rank_arg) {
-    constexpr bool FIRST = SHIFT + NBITS == 31;
-    constexpr uint32_t NB = 1u << NBITS;
-    constexpr uint32_t PER = (NB + PWG - 1) / PWG;
-    __shared__ uint32_t wsum[PWG / 64];
-    __shared__ uint32_t s_bin, s_before;
-    const uint32_t t = threadIdx.x, lane = __lane_id(), wave = t >> 6;
-    const uint32_t prefix = FIRST ? 0u : st->prefix;
-    const uint32_t rank = FIRST ? (d_rank ? *d_rank : rank_arg) : st->rank;
-    uint32_t c[PER], sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t td = PER * t + j;  // top-down bin index
-        c[j] = 0;
-        if (td < NB) {
-            const uint32_t b = NB - 1 - td;
-            c[j] = st->hist[b];
-            if (b == 0 && prefix == 0) c[j] += (uint32_t)extra_zeros;  // implicit zero keys
-        }
-        sum += c[j];
-    }
-    const uint32_t incl = wave_incl_scan(sum);
-    if (lane == 63) wsum[wave] = incl;
-    if (t == 0) { s_bin = 0xffffffffu; s_before = 0; }
-    __syncthreads();
-    uint32_t before = incl - sum;
-    for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
-    if (sum && rank >= before && rank - before < sum) {
-        uint32_t acc = before;
-#pragma unroll
-        for (uint32_t j = 0; j < PER; ++j) {
-            if (rank - acc < c[j]) { s_bin = NB - 1 - (PER * t + j); s_before = acc; break; }
-            acc += c[j];
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = t; i < RS_BINS; i += PWG) st->hist[i] = 0;
-    if (t == 0) {
-        const bool hit = s_bin != 0xffffffffu;
-        const uint32_t b = hit ? s_bin : 0u;  // rank out of range: degenerate
-        const uint32_t bb = hit ? s_before : 0u;
-        st->rank = rank - bb;
-        st->cnt_gt = (FIRST ? 0u : st->cnt_gt) + bb;
-        st->prefix = prefix | (b << SHIFT);
-        st->mask = (FIRST ? 0u : st->mask) | ((NB - 1) << SHIFT);
-    }
-}
 
 template <int SHIFT, int NBITS>
 __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size_t m, uint32_t last_mask,
-                                               RSel *st, uint64_t extra_zeros) {
+                                               RSel *st, uint64_t extra_zeros, uint32_t rank) {
     constexpr bool FIRST = SHIFT + NBITS == 31;
     constexpr uint32_t NB = 1u << NBITS;
     __shared__ uint32_t h[NCOPY][NB];
@@ -136,23 +78,30 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
         uint32_t c = 0;
 #pragma unroll
         for (uint32_t q = 0; q < NCOPY; ++q) c += h[q][i];
-        if (c) atomicAdd(&st->hist[i], c);
+        if (c) g_add(&st->hist[i], c);
     }
+    if (last_workgroup(st)) pick_level<SHIFT, NBITS, HWG>(st, extra_zeros, rank);
 }
 
 }  // namespace
 
-hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros,
-                               const uint32_t *d_rank, uint32_t rank, const DevWS &ws, int num_cu,
-                               hipStream_t s) {
+hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros, uint32_t rank,
+                               const DevWS &ws, int num_cu, hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
     const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
-    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
-    rs_pick<20, 11><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
-    rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
-    rs_pick<9, 11><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
-    rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros);
-    rs_pick<0, 9><<<1, PWG, 0, s>>>(ws.rsel, extra_zeros, d_rank, rank);
+    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
+    rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
+    rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
+    return hipGetLastError();
+}
+
+// The select's first level alone (top 11 bits; the histogram table is zero
+// afterwards) -- top-k's superset passes take it from there.
+hipError_t launch_radix_level1(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros, uint32_t rank,
+                               const DevWS &ws, int num_cu, hipStream_t s) {
+    const size_t work = (m / 4 + HWG - 1) / HWG;
+    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
+    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
     return hipGetLastError();
 }
 

@@ -14,56 +14,29 @@
 // index order.  compress() returns the capacity (topk.cpp:25) and throws when
 // capacity < k (topk.cpp:33-34).
 //
-// GPU structure: exact radix select of the k-th magnitude (select.hip), then
-// a per-tile count of (> T, == T) and an ordered emission pass.
+// GPU structure: two passes over the bucket, the rest over a 3 % superset:
+//   rs_hist level 1 (select.hip; its last workgroup picks): the top 11 bits
+//     of the k-th magnitude T;
+//   tk_pass: every element at or above that bin goes, in index order, to its
+//     tile's superset region (an overflowing tile keeps only a count and is
+//     re-read later); the bin's elements fill the level-2 histogram;
+//   tk_pick level 2, tk_hist3 + tk_pick level 3 over the supersets: T exactly;
+//   tk_count2 + tk_scan: per-tile (> T, == T) counts and their prefixes;
+//   tk_emit2: the ordered emission from the supersets.
 #include <algorithm>
 
+#include "select.h"
 #include "tile.h"
 
 namespace stg {
 
 namespace {
 
-// Per tile: elements > T and == T.
-template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) tk_count(const float *__restrict__ a, size_t m, uint32_t last_mask,
-                                                   const RSel *__restrict__ rs, uint32_t *__restrict__ tile_gt,
-                                                   uint32_t *__restrict__ tile_eq) {
-    __shared__ uint32_t s_c[2 * STG_WAVES];
-    const uint32_t T = rs->prefix;
-    const size_t base = (size_t)blockIdx.x * TV_TILE;
-    float4 v[TILE_U];
-    load_tile<VEC>(a, m, base, last_mask, v);
-    uint32_t gt = 0, eq = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < TILE_U; ++u) {
-        const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t key = f2u(comp(v[u], j)) & 0x7fffffffu;
-            const bool valid = e + j < m;
-            gt += valid && key > T;
-            eq += valid && key == T;
-        }
-    }
-    gt = wave_sum(gt);
-    eq = wave_sum(eq);
-    if (__lane_id() == 0) { s_c[threadIdx.x >> 6] = gt; s_c[STG_WAVES + (threadIdx.x >> 6)] = eq; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t g = 0, q = 0;
-        for (uint32_t w = 0; w < STG_WAVES; ++w) { g += s_c[w]; q += s_c[STG_WAVES + w]; }
-        tile_gt[blockIdx.x] = g;
-        tile_eq[blockIdx.x] = q;
-    }
-}
-
-// One workgroup: the tile counts' exclusive prefixes at [ntiles + t], the
-// totals at [2 ntiles] (a done-counter in tk_count would have 2048 workgroups
-// contend on one atomic).  2048 tiles per round, 8 consecutive per thread,
-// all loads issued before the scan.
-__global__ void __launch_bounds__(STG_WG) tk_scan(uint32_t *__restrict__ tile_gt, uint32_t *__restrict__ tile_eq,
-                                                  uint32_t ntiles) {
+// The tile counts' exclusive prefixes at [ntiles + t], the totals at
+// [2 ntiles], by the last workgroup of tk_count2 (coherent loads: the other
+// workgroups wrote the counts in this launch).  8 consecutive tiles per
+// thread, all loads issued before the scan.
+__device__ void scan_tiles(uint32_t *__restrict__ tile_gt, uint32_t *__restrict__ tile_eq, uint32_t ntiles) {
     __shared__ uint32_t sh[STG_WAVES + 1];
     uint32_t cg = 0, ce = 0;  // running prefixes
     constexpr uint32_t PT = 8;
@@ -72,8 +45,8 @@ __global__ void __launch_bounds__(STG_WG) tk_scan(uint32_t *__restrict__ tile_gt
         uint32_t g[PT], q[PT], sg = 0, sq = 0;
 #pragma unroll
         for (uint32_t i = 0; i < PT; ++i) {
-            g[i] = tb + i < ntiles ? tile_gt[tb + i] : 0u;
-            q[i] = tb + i < ntiles ? tile_eq[tb + i] : 0u;
+            g[i] = tb + i < ntiles ? ld_sc1(&tile_gt[tb + i]) : 0u;
+            q[i] = tb + i < ntiles ? ld_sc1(&tile_eq[tb + i]) : 0u;
         }
 #pragma unroll
         for (uint32_t i = 0; i < PT; ++i) { sg += g[i]; sq += q[i]; }
@@ -98,6 +71,141 @@ __global__ void __launch_bounds__(STG_WG) tk_scan(uint32_t *__restrict__ tile_gt
     }
 }
 
+constexpr uint32_t SUP_CAP = TOPK_SUP_CAP;  // superset entries kept per tile (4 per thread); more: re-read the tile
+static_assert(SUP_CAP == 4 * STG_WG, "four superset entries per thread");
+
+__device__ __forceinline__ uint32_t mag(uint32_t bits) { return bits & 0x7fffffffu; }
+
+// Pass 2: the tile's superset (|x| bits >= lo, the level-1 bin's low edge) in
+// index order as {element, raw bits}, its count, and the level-2 histogram
+// (next 11 bits) of the level-1 bin's elements.
+template <bool VEC>
+__global__ void __launch_bounds__(STG_WG) tk_pass(const float *__restrict__ a, size_t m, uint32_t last_mask,
+                                                  RSel *__restrict__ rs, uint2 *__restrict__ sup,
+                                                  uint32_t *__restrict__ sup_n) {
+    __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
+    const uint32_t lo = rs->prefix;  // level 1: bits 30..20 of T, the rest 0
+    if (blockIdx.x == 0 && threadIdx.x == 0) rs->pad[0] = lo;  // for the later passes (nothing else uses pad)
+    const uint32_t tile = blockIdx.x;
+    const size_t base = (size_t)tile * TV_TILE;
+    float4 v[TILE_U];
+    load_tile<VEC>(a, m, base, last_mask, v);
+    uint32_t q = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < TILE_U; ++u) {
+        const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t key = mag(f2u(comp(v[u], j)));
+            if (e + j < m && key >= lo) {
+                q |= 1u << (u * 4 + j);
+                // the level-1 bin's ~2 % straight to the level-2 table
+                if ((key >> 20) == (lo >> 20)) g_add(&rs->hist[(key >> 9) & 2047u], 1u);
+            }
+        }
+    }
+    uint32_t slot[TILE_U * 4], tot;
+    tile_ranks(q, slot, s_wt, &tot);
+    if (tot <= SUP_CAP) {
+        uint2 *dst = sup + (size_t)tile * SUP_CAP;
+#pragma unroll
+        for (uint32_t u = 0; u < TILE_U; ++u) {
+            const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((q >> (u * 4 + j)) & 1u) dst[slot[u * 4 + j]] = make_uint2((uint32_t)(e + j), f2u(comp(v[u], j)));
+        }
+    }
+    if (threadIdx.x == 0) sup_n[tile] = tot;
+}
+
+// The tile's superset entries (or, for a tile that overflowed, its elements
+// re-read with the same keys) handed one at a time to f(element, raw bits)
+// in index order per thread: thread t takes entries 4t .. 4t+3.
+template <bool VEC, typename F>
+__device__ __forceinline__ void for_tile(const float *__restrict__ a, size_t m, uint32_t last_mask, uint32_t lo,
+                                         const uint2 *__restrict__ sup, uint32_t n, F f) {
+    const uint32_t tile = blockIdx.x;
+    if (n <= SUP_CAP) {
+        const uint2 *src = sup + (size_t)tile * SUP_CAP;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t j = 4 * threadIdx.x + r;
+            if (j < n) {
+                const uint2 x = src[j];
+                f(x.x, x.y);
+            }
+        }
+        return;
+    }
+    const size_t base = (size_t)tile * TV_TILE;
+    float4 v[TILE_U];
+    load_tile<VEC>(a, m, base, last_mask, v);
+#pragma unroll
+    for (uint32_t u = 0; u < TILE_U; ++u) {
+        const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (e + j < m && mag(f2u(comp(v[u], j))) >= lo) f((uint32_t)(e + j), f2u(comp(v[u], j)));
+    }
+}
+
+// Level 3 over the supersets: the low 9 bits of the keys in the level-2 bin.
+template <bool VEC>
+__global__ void __launch_bounds__(STG_WG) tk_hist3(const float *__restrict__ a, size_t m, uint32_t last_mask,
+                                                   RSel *__restrict__ rs, const uint2 *__restrict__ sup,
+                                                   const uint32_t *__restrict__ sup_n) {
+    __shared__ uint32_t h3[512];
+    for (uint32_t i = threadIdx.x; i < 512; i += STG_WG) h3[i] = 0;
+    const uint32_t prefix = rs->prefix, mask = rs->mask, lo = rs->pad[0];  // bits 30..9
+    const uint32_t n = sup_n[blockIdx.x];
+    __syncthreads();
+    for_tile<VEC>(a, m, last_mask, lo, sup, n, [&](uint32_t, uint32_t bits) {
+        const uint32_t key = mag(bits);
+        if ((key & mask) == prefix) atomicAdd(&h3[key & 511u], 1u);
+    });
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 512; i += STG_WG)
+        if (h3[i]) g_add(&rs->hist[i], h3[i]);
+}
+
+// A level's pick as its own launch (the per-tile passes have too many
+// workgroups for a last-workgroup pick to pay).
+template <int SHIFT, int NBITS>
+__global__ void __launch_bounds__(1024) tk_pick(RSel *rs, uint64_t zeros) {
+    pick_level<SHIFT, NBITS, 1024>(rs, zeros, 0);
+}
+
+__global__ void __launch_bounds__(STG_WG) tk_scan(uint32_t *tile_gt, uint32_t *tile_eq, uint32_t ntiles) {
+    scan_tiles(tile_gt, tile_eq, ntiles);
+}
+
+// Per tile: elements > T and == T.
+template <bool VEC>
+__global__ void __launch_bounds__(STG_WG) tk_count2(const float *__restrict__ a, size_t m, uint32_t last_mask,
+                                                    const RSel *__restrict__ rs,
+                                                    const uint2 *__restrict__ sup, const uint32_t *__restrict__ sup_n,
+                                                    uint32_t *__restrict__ tile_gt, uint32_t *__restrict__ tile_eq) {
+    __shared__ uint32_t s_c[2 * STG_WAVES];
+    const uint32_t T = rs->prefix, lo = rs->pad[0];
+    uint32_t gt = 0, eq = 0;
+    for_tile<VEC>(a, m, last_mask, lo, sup, sup_n[blockIdx.x], [&](uint32_t, uint32_t bits) {
+        const uint32_t key = mag(bits);
+        gt += key > T;
+        eq += key == T;
+    });
+    gt = wave_sum(gt);
+    eq = wave_sum(eq);
+    if (__lane_id() == 0) { s_c[threadIdx.x >> 6] = gt; s_c[STG_WAVES + (threadIdx.x >> 6)] = eq; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t g = 0, e = 0;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) { g += s_c[w]; e += s_c[STG_WAVES + w]; }
+        tile_gt[blockIdx.x] = g;
+        tile_eq[blockIdx.x] = e;
+    }
+}
+
 struct TkArgs {
     const float *a;
     uint64_t m;          // elements actually present
@@ -112,53 +220,88 @@ struct TkArgs {
     const RSel *rs;
     const uint32_t *tile_gt;
     const uint32_t *tile_eq;
+    const uint2 *sup;
+    const uint32_t *sup_n;
 };
 
 // One workgroup per tile: the winners (> T, then == T in index order until
-// k) at their prefix offsets.
+// k) at their prefix offsets, from the tile's superset.
 template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) tk_emit(TkArgs a) {
-    __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
+__global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
+    __shared__ uint32_t sh[STG_WAVES + 1];
     const uint32_t tile = blockIdx.x, tid = threadIdx.x, nt = a.ntiles;
     const uint32_t T = a.rs->prefix;
     const uint64_t need_eq = (uint64_t)a.k - a.rs->cnt_gt;  // ties to take, in index order
     const uint32_t cg = a.tile_gt[tile], ce = a.tile_eq[tile];
     const uint64_t gt_before = a.tile_gt[nt + tile], eq_before = a.tile_eq[nt + tile];
     if (cg || (ce && eq_before < need_eq)) {  // uniform per workgroup
-        float4 v[TILE_U];
-        const size_t base = (size_t)tile * TV_TILE;
-        load_tile<VEC>(a.a, a.m, base, a.last_mask, v);
-        uint32_t qg = 0, qe = 0;
+        const uint32_t n = a.sup_n[tile];
+        if (n <= SUP_CAP) {
+            // four consecutive entries per thread: ranks by two workgroup scans
+            const uint2 *src = a.sup + (size_t)tile * SUP_CAP;
+            uint2 x[4];
+            uint32_t qe = 0, qg = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < TILE_U; ++u) {
-            const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+            for (uint32_t r = 0; r < 4; ++r) {
+                const uint32_t j = 4 * tid + r;
+                x[r] = j < n ? src[j] : make_uint2(0u, 0u);
+                const uint32_t key = mag(x[r].y);
+                if (j < n && key > T) qg |= 1u << r;
+                if (j < n && key == T) qe |= 1u << r;
+            }
+            uint32_t tot;
+            uint32_t er = wg_excl_scan((uint32_t)__popc(qe), sh, &tot);
+            uint32_t qw = qg;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t key = f2u(comp(v[u], j)) & 0x7fffffffu;
-                if (e + j < a.m) {
-                    if (key > T) qg |= 1u << (u * 4 + j);
-                    else if (key == T) qe |= 1u << (u * 4 + j);
+            for (uint32_t r = 0; r < 4; ++r)
+                if ((qe >> r) & 1u) { if (eq_before + er < need_eq) qw |= 1u << r; ++er; }
+            uint32_t wr = wg_excl_scan((uint32_t)__popc(qw), sh, &tot);
+            const uint64_t win_before = gt_before + std::min(eq_before, need_eq);
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r) {
+                if ((qw >> r) & 1u) {
+                    const uint64_t slot = win_before + wr++;
+                    a.idx[slot] = a.bug_compat ? (uint32_t)slot : x[r].x + (uint32_t)a.idx_offset;
+                    a.val[slot] = u2f(x[r].y);
                 }
             }
-        }
-        uint32_t se[TILE_U * 4], sw[TILE_U * 4], tot;
-        tile_ranks(qe, se, s_wt, &tot);
-        uint32_t qw = qg;
+        } else {  // the tile overflowed its superset: from the bucket itself
+            __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
+            float4 v[TILE_U];
+            const size_t base = (size_t)tile * TV_TILE;
+            load_tile<VEC>(a.a, a.m, base, a.last_mask, v);
+            uint32_t qg = 0, qe = 0;
 #pragma unroll
-        for (uint32_t b = 0; b < TILE_U * 4; ++b)
-            if (((qe >> b) & 1u) && eq_before + se[b] < need_eq) qw |= 1u << b;
-        tile_ranks(qw, sw, s_wt, &tot);
-        const uint64_t win_before = gt_before + std::min(eq_before, need_eq);
+            for (uint32_t u = 0; u < TILE_U; ++u) {
+                const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
 #pragma unroll
-        for (uint32_t u = 0; u < TILE_U; ++u) {
-            const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t key = mag(f2u(comp(v[u], j)));
+                    if (e + j < a.m) {
+                        if (key > T) qg |= 1u << (u * 4 + j);
+                        else if (key == T) qe |= 1u << (u * 4 + j);
+                    }
+                }
+            }
+            uint32_t se[TILE_U * 4], sw[TILE_U * 4], tot;
+            tile_ranks(qe, se, s_wt, &tot);
+            uint32_t qw = qg;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t b = u * 4 + j;
-                if ((qw >> b) & 1u) {
-                    const uint64_t slot = win_before + sw[b];
-                    a.idx[slot] = a.bug_compat ? (uint32_t)slot : (uint32_t)(e + j) + (uint32_t)a.idx_offset;
-                    a.val[slot] = comp(v[u], j);
+            for (uint32_t b = 0; b < TILE_U * 4; ++b)
+                if (((qe >> b) & 1u) && eq_before + se[b] < need_eq) qw |= 1u << b;
+            tile_ranks(qw, sw, s_wt, &tot);
+            const uint64_t win_before = gt_before + std::min(eq_before, need_eq);
+#pragma unroll
+            for (uint32_t u = 0; u < TILE_U; ++u) {
+                const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t b = u * 4 + j;
+                    if ((qw >> b) & 1u) {
+                        const uint64_t slot = win_before + sw[b];
+                        a.idx[slot] = a.bug_compat ? (uint32_t)slot : (uint32_t)(e + j) + (uint32_t)a.idx_offset;
+                        a.val[slot] = comp(v[u], j);
+                    }
                 }
             }
         }
@@ -193,13 +336,21 @@ hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s) {
         zeros = a.n - m;
     }
     const uint32_t kk = (uint32_t)std::min<uint64_t>(a.k, a.n);
-    if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    hipError_t e = launch_radix_select(a.src, m, last_mask, zeros, nullptr, kk - 1, ws, a.num_cu, s);
-    if (e != hipSuccess) return e;
     const uint32_t ntiles = (uint32_t)((m + TV_TILE - 1) / TV_TILE);
     const bool vec = (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0;
-    if (vec) tk_count<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, ws.tile_cnt, ws.tile_aux);
-    else tk_count<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, ws.tile_cnt, ws.tile_aux);
+    uint2 *sup = reinterpret_cast<uint2 *>(ws.sums);          // ntiles x SUP_CAP entries
+    uint32_t *sup_n = ws.tile_cnt + 2 * (size_t)ntiles + 1;  // after the > T counts and their prefixes
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    hipError_t e = launch_radix_level1(a.src, m, last_mask, zeros, kk - 1, ws, a.num_cu, s);
+    if (e != hipSuccess) return e;
+    if (vec) tk_pass<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
+    else tk_pass<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
+    tk_pick<9, 11><<<1, 1024, 0, s>>>(ws.rsel, zeros);
+    if (vec) tk_hist3<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
+    else tk_hist3<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
+    tk_pick<0, 9><<<1, 1024, 0, s>>>(ws.rsel, zeros);
+    if (vec) tk_count2<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux);
+    else tk_count2<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux);
     tk_scan<<<1, STG_WG, 0, s>>>(ws.tile_cnt, ws.tile_aux, ntiles);
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
     TkArgs t;
@@ -218,8 +369,10 @@ hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s) {
     t.rs = ws.rsel;
     t.tile_gt = ws.tile_cnt;
     t.tile_eq = ws.tile_aux;
-    if (vec) tk_emit<true><<<ntiles, STG_WG, 0, s>>>(t);
-    else tk_emit<false><<<ntiles, STG_WG, 0, s>>>(t);
+    t.sup = sup;
+    t.sup_n = sup_n;
+    if (vec) tk_emit2<true><<<ntiles, STG_WG, 0, s>>>(t);
+    else tk_emit2<false><<<ntiles, STG_WG, 0, s>>>(t);
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
     return hipGetLastError();
 }

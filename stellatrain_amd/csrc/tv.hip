@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(TWG) tv_fill(TvFillArgs a) {
 hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     if (a.first) {
         const uint32_t rank = (uint32_t)std::min<uint64_t>(a.k, a.n - 1);
-        hipError_t e = launch_radix_select(a.src, a.n, 0xffffffffu, 0, nullptr, rank, ws, a.num_cu, s);
+        hipError_t e = launch_radix_select(a.src, a.n, 0xffffffffu, 0, rank, ws, a.num_cu, s);
         if (e != hipSuccess) return e;
         tv_init_state<<<1, 1, 0, s>>>(a.state, ws.rsel);
     }

@@ -722,7 +722,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             const uint32_t nblk = (uint32_t)((b.n + 15) / 16);
             tv16_seq_sums<<<(nblk + STG_WG - 1) / STG_WG, STG_WG, 0, s>>>(b.src, b.n, b.sums, nblk);
             const uint32_t bk = std::min<uint32_t>(b.k / 16, nblk - 1);
-            hipError_t e = launch_radix_select(b.sums, nblk, 0xffffffffu, 0, nullptr, bk, ws, a.num_cu, s);
+            hipError_t e = launch_radix_select(b.sums, nblk, 0xffffffffu, 0, bk, ws, a.num_cu, s);
             if (e != hipSuccess) return e;
             tv16_init_state<<<1, 1, 0, s>>>(b.state, ws.rsel);
         }

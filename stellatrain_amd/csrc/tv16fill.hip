@@ -431,7 +431,6 @@ tv16_fill(Tv16FillArgs A) {
         if (!(k > 0.f)) return NBIN - 1;
         return min((tb - 1u - kb) >> 8, NBIN - 1);
     };
-    auto obin = [&](uint32_t e) -> uint32_t { return kbin(key[e]); };
     auto okey = [&](uint32_t e) -> uint64_t { return (uint64_t)(~ford(u2f(key[e]))) << 32; };
     auto ksum = [&](uint32_t r) -> float { return u2f(key[S.ord[r]]); };  // sum at rank r
     uint32_t W = 0, Et = NONE;  // entries kept, the ragged tail's element id

@@ -14,6 +14,7 @@ constexpr uint32_t TV16_WIN = 1u << 18;      // regime-B window below t, in ulps
 constexpr uint32_t TV16_SCAN_LDS = 35584;     // LDS bytes of a scan workgroup (bound; tv16.hip checks)
 
 constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)
+constexpr uint32_t TOPK_SUP_CAP = 1024;      // top-k superset entries kept per tile
 constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
 constexpr uint32_t TV_SCAP = 2048;           // threshold-v qualifiers listed per range
 
@@ -64,8 +65,9 @@ struct RSel {
     uint32_t mask;      // which bits are fixed
     uint32_t rank;      // remaining rank (0-based, descending) inside the prefix
     uint32_t cnt_gt;    // keys strictly above the prefix range
-    uint32_t done;      // workgroups done with the current level (the last one picks)
-    uint32_t pad[3];
+    uint32_t done;      // classes of workgroups done with the current pass (the last one picks)
+    uint32_t pad[3];    // pad[0]: top-k's superset floor
+    uint32_t done8[8];  // workgroups done, per class blockIdx.x % 8
     uint32_t hist[RS_BINS];
 };
 
@@ -167,9 +169,10 @@ hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s);
 // i < m, with the last element's bits additionally masked by `last_mask`, plus
 // `extra_zeros` implicit zero keys.  Result in ws.rsel (prefix = key bits,
 // cnt_gt = keys strictly greater, rank = rank among equal keys).
-hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros,
-                               const uint32_t *d_rank, uint32_t rank, const DevWS &ws, int num_cu,
-                               hipStream_t s);
+hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros, uint32_t rank,
+                               const DevWS &ws, int num_cu, hipStream_t s);
+hipError_t launch_radix_level1(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros, uint32_t rank,
+                               const DevWS &ws, int num_cu, hipStream_t s);
 
 hipError_t launch_synth(float *dst, size_t n, uint64_t seed, int dist, uint32_t param, hipStream_t s);
 
