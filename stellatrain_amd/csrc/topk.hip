@@ -83,14 +83,21 @@ template <bool VEC>
 __global__ void __launch_bounds__(STG_WG) tk_pass(const float *__restrict__ a, size_t m, uint32_t last_mask,
                                                   RSel *__restrict__ rs, uint2 *__restrict__ sup,
                                                   uint32_t *__restrict__ sup_n) {
+    constexpr uint32_t NB2 = 2048;
+    __shared__ uint32_t h2[NB2];
     __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
+    for (uint32_t i = threadIdx.x; i < NB2; i += STG_WG) h2[i] = 0;
     const uint32_t lo = rs->prefix;  // level 1: bits 30..20 of T, the rest 0
     if (blockIdx.x == 0 && threadIdx.x == 0) rs->pad[0] = lo;  // for the later passes (nothing else uses pad)
-    const uint32_t tile = blockIdx.x;
+    __syncthreads();
+    const uint32_t tile = blockIdx.x, lane = __lane_id(), wave = threadIdx.x >> 6;
     const size_t base = (size_t)tile * TV_TILE;
     float4 v[TILE_U];
     load_tile<VEC>(a, m, base, last_mask, v);
-    uint32_t q = 0;
+    // flags, the level-2 histogram, and each lane's place among the flagged
+    // elements of its wave for each u (element order is (u, wave, lane, j));
+    // slots are rebuilt from these when written, so no per-element registers
+    uint32_t q = 0, pre[TILE_U];
 #pragma unroll
     for (uint32_t u = 0; u < TILE_U; ++u) {
         const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
@@ -99,24 +106,39 @@ __global__ void __launch_bounds__(STG_WG) tk_pass(const float *__restrict__ a, s
             const uint32_t key = mag(f2u(comp(v[u], j)));
             if (e + j < m && key >= lo) {
                 q |= 1u << (u * 4 + j);
-                // the level-1 bin's ~2 % straight to the level-2 table
-                if ((key >> 20) == (lo >> 20)) g_add(&rs->hist[(key >> 9) & 2047u], 1u);
+                if ((key >> 20) == (lo >> 20)) atomicAdd(&h2[(key >> 9) & (NB2 - 1)], 1u);
             }
         }
+        const uint32_t c = (uint32_t)__popc((q >> (4 * u)) & 0xfu);
+        const uint32_t incl = wave_incl_scan(c);
+        pre[u] = incl - c;
+        if (lane == 63) s_wt[u * STG_WAVES + wave] = incl;
     }
-    uint32_t slot[TILE_U * 4], tot;
-    tile_ranks(q, slot, s_wt, &tot);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // (u, wave) offsets: one wave scans the 32 counts
+        constexpr uint32_t NW = TILE_U * STG_WAVES;
+        static_assert(NW <= 64, "one wave scans the wave counts");
+        const uint32_t x = threadIdx.x < NW ? s_wt[threadIdx.x] : 0u;
+        const uint32_t inc = wave_incl_scan(x);
+        if (threadIdx.x < NW) s_wt[threadIdx.x] = inc - x;
+        if (threadIdx.x == NW - 1) s_wt[NW] = inc;
+    }
+    __syncthreads();
+    const uint32_t tot = s_wt[TILE_U * STG_WAVES];
     if (tot <= SUP_CAP) {
         uint2 *dst = sup + (size_t)tile * SUP_CAP;
 #pragma unroll
         for (uint32_t u = 0; u < TILE_U; ++u) {
             const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
+            uint32_t slot = s_wt[u * STG_WAVES + wave] + pre[u];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                if ((q >> (u * 4 + j)) & 1u) dst[slot[u * 4 + j]] = make_uint2((uint32_t)(e + j), f2u(comp(v[u], j)));
+                if ((q >> (u * 4 + j)) & 1u) dst[slot++] = make_uint2((uint32_t)(e + j), f2u(comp(v[u], j)));
         }
     }
     if (threadIdx.x == 0) sup_n[tile] = tot;
+    for (uint32_t i = threadIdx.x; i < NB2; i += STG_WG)
+        if (h2[i]) g_add(&rs->hist[i], h2[i]);
 }
 
 // The tile's superset entries (or, for a tile that overflowed, its elements
