@@ -167,6 +167,15 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
 __device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
     __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Zero 16 bytes at byte offset `off` (per lane, 16-byte aligned) of the
+// uniform region [base, base + bytes) with an sc1 buffer store: the line goes
+// to the device-coherent level like st_sc1, one write instead of four.
+__device__ __forceinline__ void st_sc1_zero16(uint32_t *base, uint32_t bytes, uint32_t off) {
+    typedef unsigned int zv4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+    const zv4 z = {0u, 0u, 0u, 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(z, r, off, 0, 16 /* sc1 */);
+}
 // Global (agent-scope, relaxed) atomic add / or; return the old value.
 __device__ __forceinline__ uint32_t g_add(uint32_t *p, uint32_t v) {
     return __hip_atomic_fetch_add(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -15,8 +15,9 @@ namespace stg {
 // afresh.  Run by the last workgroup of the pass that filled the histogram
 // (the other workgroups' bin atomics are device-visible: they fenced before
 // counting themselves done), so a level costs no launch of its own.
-template <int SHIFT, int NBITS, uint32_t NT>
+template <int SHIFT, int NBITS, uint32_t NT, uint32_t NSH>
 __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
+    static_assert(NSH >= 1 && NSH <= RS_SHARDS, "shards the feeding pass added into");
     constexpr bool FIRST = SHIFT + NBITS == 31;
     constexpr uint32_t NB = 1u << NBITS;
     constexpr uint32_t PER = (NB + NT - 1) / NT;
@@ -32,7 +33,9 @@ __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
         c[j] = 0;
         if (td < NB) {
             const uint32_t b = NB - 1 - td;
-            c[j] = ld_sc1(&st->hist[b]);
+            c[j] = 0;
+#pragma unroll
+            for (uint32_t h = 0; h < NSH; ++h) c[j] += ld_sc1(&st->hist[h][b]);
             if (b == 0 && prefix == 0) c[j] += (uint32_t)extra_zeros;  // implicit zero keys
         }
         sum += c[j];
@@ -52,7 +55,13 @@ __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
         }
     }
     __syncthreads();
-    for (uint32_t i = t; i < RS_BINS; i += NT) st_sc1(&st->hist[i], 0u);
+    // zero the shards' bins read above, 16 bytes per store (sc1: straight to
+    // the device-coherent level, where the next pass's atomics land)
+    static_assert(NB % 4 == 0, "whole 16-byte groups");
+    for (uint32_t i = t; i < NSH * (NB / 4); i += NT) {
+        const uint32_t h = i / (NB / 4), g = i % (NB / 4);
+        st_sc1_zero16(&st->hist[0][0], NSH * RS_BINS * 4u, (h * RS_BINS + 4 * g) * 4u);
+    }
     if (t == 0) {
         const bool hit = s_bin != 0xffffffffu;
         const uint32_t b = hit ? s_bin : 0u;  // rank out of range: degenerate
@@ -67,21 +76,22 @@ __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
 // True in exactly one workgroup of the grid: the last to finish this pass.
 // What the last one reads was written with agent-scope atomics or stores
 // (coherent across the XCDs' L2s), and every thread's memory operations have
-// completed before its workgroup counts itself done.  Counting is two-level -- the workgroups of
-// each residue class of blockIdx.x mod 8 (the XCD round robin) on their own
-// word, the last of each class on the shared one -- so no word takes more
-// than gridDim.x / 8 atomics.
+// completed before its workgroup counts itself done.  Counting is two-level --
+// the workgroups of each residue class of blockIdx.x mod 64 on their own word,
+// the last of each class on the shared one -- so no word takes more than
+// gridDim.x / 64 returning atomics (one word serialises them at ~90 per us).
 __device__ inline bool last_workgroup(RSel *st) {
     __shared__ uint32_t s_last;
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt / lgkmcnt / expcnt all 0: this thread's memory ops are done
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t G = gridDim.x, c = blockIdx.x & 7u;
-        const uint32_t in_c = G / 8 + (c < G % 8 ? 1u : 0u);  // workgroups of this class
+        constexpr uint32_t NC = 64;
+        const uint32_t G = gridDim.x, c = blockIdx.x % NC;
+        const uint32_t in_c = G / NC + (c < G % NC ? 1u : 0u);  // workgroups of this class
         uint32_t last = 0;
-        if (g_add(&st->done8[c], 1u) == in_c - 1) {
-            st_sc1(&st->done8[c], 0u);
-            const uint32_t classes = G < 8 ? G : 8u;
+        if (g_add(&st->done64[c], 1u) == in_c - 1) {
+            st_sc1(&st->done64[c], 0u);
+            const uint32_t classes = G < NC ? G : NC;
             if (g_add(&st->done, 1u) == classes - 1) {
                 st_sc1(&st->done, 0u);
                 last = 1;

@@ -32,8 +32,11 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
                                                RSel *st, uint64_t extra_zeros, uint32_t rank) {
     constexpr bool FIRST = SHIFT + NBITS == 31;
     constexpr uint32_t NB = 1u << NBITS;
-    __shared__ uint32_t h[NCOPY][NB];
-    for (uint32_t i = threadIdx.x; i < NCOPY * NB; i += HWG) (&h[0][0])[i] = 0;
+    // copies one word apart in the bank order (a stride of NB words would put
+    // every copy of a bin in the same bank)
+    constexpr uint32_t NBP = NB + 1;
+    __shared__ uint32_t h[NCOPY][NBP];
+    for (uint32_t i = threadIdx.x; i < NCOPY * NBP; i += HWG) (&h[0][0])[i] = 0;
     // the first level counts every key (its prefix and mask are still those of
     // the previous select)
     const uint32_t prefix = FIRST ? 0u : st->prefix;
@@ -51,10 +54,15 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
     constexpr uint32_t UF = 4;
     for (size_t i0 = (size_t)blockIdx.x * HWG + threadIdx.x; i0 < m4; i0 += UF * stride) {
         float4 v[UF];
+        if (i0 + (UF - 1) * stride < m4) {  // all UF loads in range: issue them together
 #pragma unroll
-        for (uint32_t u = 0; u < UF; ++u) {
-            const size_t i = i0 + u * stride;
-            v[u] = i < m4 ? a4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (uint32_t u = 0; u < UF; ++u) v[u] = a4[i0 + u * stride];
+        } else {
+#pragma unroll
+            for (uint32_t u = 0; u < UF; ++u) {
+                const size_t i = i0 + u * stride;
+                v[u] = i < m4 ? a4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
 #pragma unroll
         for (uint32_t u = 0; u < UF; ++u) {
@@ -78,9 +86,9 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
         uint32_t c = 0;
 #pragma unroll
         for (uint32_t q = 0; q < NCOPY; ++q) c += h[q][i];
-        if (c) g_add(&st->hist[i], c);
+        if (c) g_add(&st->hist[blockIdx.x % RS_SH_HIST][i], c);
     }
-    if (last_workgroup(st)) pick_level<SHIFT, NBITS, HWG>(st, extra_zeros, rank);
+    if (last_workgroup(st)) pick_level<SHIFT, NBITS, HWG, RS_SH_HIST>(st, extra_zeros, rank);
 }
 
 }  // namespace

@@ -14,6 +14,15 @@ constexpr uint32_t TILE_U = 8;  // float4 per thread per tile
 template <bool VEC>
 __device__ __forceinline__ void load_tile(const float *__restrict__ a, size_t m, size_t base, uint32_t last_mask,
                                           float4 (&v)[TILE_U]) {
+    // a whole, aligned tile with no partial float: all TILE_U loads issued
+    // before any is used (a per-load bounds test makes the compiler wait for
+    // each load in turn: TILE_U serial HBM round trips)
+    if (VEC && base + TV_TILE <= m && (last_mask == 0xffffffffu || base + TV_TILE < m)) {
+        const float4 *p = reinterpret_cast<const float4 *>(a + base) + threadIdx.x;
+#pragma unroll
+        for (uint32_t u = 0; u < TILE_U; ++u) v[u] = p[u * STG_WG];
+        return;
+    }
 #pragma unroll
     for (uint32_t u = 0; u < TILE_U; ++u) {
         const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);

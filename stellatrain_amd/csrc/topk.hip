@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(STG_WG) tk_pass(const float *__restrict__ a, s
     }
     if (threadIdx.x == 0) sup_n[tile] = tot;
     for (uint32_t i = threadIdx.x; i < NB2; i += STG_WG)
-        if (h2[i]) g_add(&rs->hist[i], h2[i]);
+        if (h2[i]) g_add(&rs->hist[blockIdx.x % RS_SHARDS][i], h2[i]);
 }
 
 // The tile's superset entries (or, for a tile that overflowed, its elements
@@ -188,14 +188,14 @@ __global__ void __launch_bounds__(STG_WG) tk_hist3(const float *__restrict__ a, 
     });
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < 512; i += STG_WG)
-        if (h3[i]) g_add(&rs->hist[i], h3[i]);
+        if (h3[i]) g_add(&rs->hist[blockIdx.x % RS_SHARDS][i], h3[i]);
 }
 
 // A level's pick as its own launch (the per-tile passes have too many
 // workgroups for a last-workgroup pick to pay).
 template <int SHIFT, int NBITS>
 __global__ void __launch_bounds__(1024) tk_pick(RSel *rs, uint64_t zeros) {
-    pick_level<SHIFT, NBITS, 1024>(rs, zeros, 0);
+    pick_level<SHIFT, NBITS, 1024, RS_SHARDS>(rs, zeros, 0);
 }
 
 __global__ void __launch_bounds__(STG_WG) tk_scan(uint32_t *tile_gt, uint32_t *tile_eq, uint32_t ntiles) {

@@ -19,6 +19,8 @@ constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) 
 constexpr uint32_t TV_SCAP = 2048;           // threshold-v qualifiers listed per range
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
+constexpr uint32_t RS_SHARDS = 8;            // histogram copies: workgroup w adds into shard w % RS_SHARDS
+constexpr uint32_t RS_SH_HIST = 4;           // ... of which rs_hist's one workgroup per CU uses the first 4
 
 // thresholdv16 in-launch control block (one launch = a batch of <= MAX_BATCH
 // buckets cut into fixed 2048-line chunks).  The per-call chunk counter comes
@@ -67,8 +69,12 @@ struct RSel {
     uint32_t cnt_gt;    // keys strictly above the prefix range
     uint32_t done;      // classes of workgroups done with the current pass (the last one picks)
     uint32_t pad[3];    // pad[0]: top-k's superset floor
-    uint32_t done8[8];  // workgroups done, per class blockIdx.x % 8
-    uint32_t hist[RS_BINS];
+    uint32_t done64[64];  // workgroups done, per class blockIdx.x % 64
+    // The level histogram in RS_SHARDS copies, summed by the pick: device-scope
+    // atomics on one word serialise at the memory side (~90 per us), so a
+    // 2048-workgroup pass adding into one copy spent ~15 us on its hot bins
+    // (into 8 copies: 256 adds per word, spread over the pass).
+    uint32_t hist[RS_SHARDS][RS_BINS];
 };
 
 struct DevWS {
