@@ -54,6 +54,12 @@ struct Workspace {
     void *fixed = nullptr;
     size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0, cap_desc = 0;
     uint32_t epoch = 0;  // thresholdv16 call counter (hand-off tags)
+    // threshold-v: the ticket's value at the next call, the last call's
+    // range-descriptor tag and the descriptor block last zeroed (tile_cnt, its size)
+    uint64_t tv_base = 0;
+    uint32_t tv_tag = 0;
+    uint32_t *tv_desc = nullptr;
+    size_t tv_desc_cap = 0;
     // device buffers of the host-memory entry point
     float *h_src = nullptr;
     size_t cap_src = 0;
@@ -93,6 +99,7 @@ struct Workspace {
         const size_t o_fail = carve(sizeof(uint32_t));
         const size_t o_cand = carve(sizeof(uint32_t) * stg::CAND_WORDS * stg::MAX_BATCH);
         const size_t o_misc = carve(sizeof(uint32_t) * 64);
+        const size_t o_tvt = carve(sizeof(uint64_t));
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
         // control block are ordered after it (a plain hipMemset runs on the
@@ -105,6 +112,7 @@ struct Workspace {
         d.fail = reinterpret_cast<uint32_t *>(b + o_fail);
         d.cand = reinterpret_cast<uint32_t *>(b + o_cand);
         d.misc = reinterpret_cast<uint32_t *>(b + o_misc);
+        d.tv_ticket = reinterpret_cast<uint64_t *>(b + o_tvt);
         return STG_OK;
     }
 
@@ -482,9 +490,19 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         KeyState *st;
         bool fresh;
         if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
-        if ((rc = ws->ensure(1, stg::TV_MAXG, (size_t)stg::TV_MAXG * stg::TV_SCAP))) return rc;
-        stg::TvLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, d_count, st, fresh, h->num_cu, ev};
+        // range descriptors: two words per range at tile_cnt, maxima at tile_aux
+        if ((rc = ws->ensure(1, 2 * (size_t)stg::TV_MAXG, 1))) return rc;
+        if (ws->tv_desc != ws->d.tile_cnt || ws->tv_desc_cap != ws->cap_tiles) {  // fresh memory: no stale tags
+            HIP_TRY(hipMemsetAsync(ws->d.tile_cnt, 0, ws->cap_tiles * sizeof(uint32_t), s));
+            ws->tv_desc = ws->d.tile_cnt;
+            ws->tv_desc_cap = ws->cap_tiles;
+        }
+        if (++ws->tv_tag == 0) ws->tv_tag = 1;
+        uint32_t grid = 0;
+        stg::TvLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, d_count, st, fresh, h->num_cu, ev,
+                        ws->tv_tag, ws->tv_base, &grid};
         HIP_TRY(stg::launch_tv(a, ws->d, s));
+        ws->tv_base += grid;
     } else {
         const size_t ntiles = (n + stg::TV_TILE - 1) / stg::TV_TILE;
         // superset entries (two words each, stg::TOPK_SUP_CAP per tile); per-tile

@@ -10,17 +10,17 @@
 // k < cnt -> t = fma(0.01*cnt/k, gmax, t) in double (GCC contracts it at -O3).
 // Returns min(cnt, cap).  The state is keyed by the src pointer (:44).
 //
-// GPU structure (two launches, both HBM-bound):
-//   tv_scan  persistent, 1024-thread workgroups (2 per CU), each owning a
-//            contiguous range of the bucket: 16 waves stream it with a rolling
-//            pipeline of SCAN_D nontemporal float4 loads per lane, count the
-//            qualifiers and max|x|, and list the qualifiers (position, value)
-//            in LDS; at the end the list is put in position order (a counting
-//            rank over the list) and written to the workgroup's staging slot.
-//   tv_fill  one workgroup per range: the prefix of the ranges' counts places
-//            the range's sorted list in the output (capped); workgroup 0 folds
-//            the maxima and writes the AIMD threshold and the count.  A range
-//            whose list overflowed its LDS capacity is re-scanned in order.
+// GPU structure: one launch, HBM-bound (tv_pass).  1024-thread workgroups (2
+// per CU) take contiguous ranges of the bucket in ticket order; 16 waves
+// stream the range with a rolling pipeline of SCAN_D nontemporal float4 loads
+// per lane, count the qualifiers and max|x|, and list the qualifiers
+// (position, value) in LDS; the range publishes its count, sums the counts of
+// the earlier ranges (look-back: taken earlier, so their workgroups are
+// running or done; no co-residency needed) and writes its list in position
+// order at that offset
+// (capped).  A range whose list overflowed its LDS capacity is re-scanned in
+// order.  The last range folds the counts and maxima into the AIMD threshold
+// and the count.
 #include <algorithm>
 
 #include "ws.h"
@@ -55,25 +55,49 @@ __device__ __forceinline__ TvRange tv_range(uint64_t n4, uint32_t G, uint32_t w)
     return r;
 }
 
-__global__ void __launch_bounds__(TWG, 8) tv_scan(const float *__restrict__ src, uint64_t n,
-                                                   const KeyState *__restrict__ state, uint32_t *__restrict__ wg_cnt,
-                                                   uint32_t *__restrict__ wg_max, uint32_t *__restrict__ stage_pos,
-                                                   float *__restrict__ stage_val, CallParams *cp) {
+struct TvArgs {
+    const float *src;
+    uint64_t n;
+    uint32_t k, cap;
+    uint32_t *idx;
+    float *val;
+    uint32_t *count_out;
+    KeyState *state;
+    uint64_t *desc;      // per range: {call tag:32 | qualifier count:32}
+    uint32_t *rmax;      // per range: max |x| bits (stored before the range's desc)
+    uint32_t tag;        // this call's tag, >= 1
+    uint64_t *ticket;    // ranges taken: monotonic over the workspace's calls (zero at creation)
+    uint64_t base;       // its value when this call starts (G per earlier call)
+    uint32_t *fail;      // the workspace's sticky failure word
+};
+
+// One launch: the workgroup with ticket r streams range r, publishes its count,
+// sums the counts of the earlier ranges (look-back) and writes the range's
+// qualifiers at that offset in position order; range G-1 folds the counts and
+// maxima into the AIMD threshold and the count.
+__global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     __shared__ uint32_t s_pos[LCAP];
     __shared__ float s_val[LCAP];
-    __shared__ uint32_t s_n, s_cnt[TNW], s_max[TNW];
-    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
+    __shared__ uint32_t s_n, s_r, s_cnt[TNW], s_max[TNW];
+    __shared__ uint64_t s_P;
+    __shared__ uint32_t sh[TNW + 1];
+    const uint32_t G = gridDim.x, tid = threadIdx.x;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const float t = state->t;
-    if (w == 0 && tid == 0) cp->t = t;  // the fill kernel reads t from here
-    if (tid == 0) s_n = 0;
+    if (tid == 0) {
+        s_n = 0;
+        s_r = (uint32_t)(g_add(a.ticket, 1ull) - a.base);
+    }
+    // read before this range's count is published: the last workgroup
+    // rewrites the state only after every range's count is in
+    const float t = a.state->t;
     __syncthreads();
-    const uint64_t n4 = n / 4;
-    const TvRange R = tv_range(n4, G, w);
+    const uint32_t r = s_r;  // ranges in ticket order
+    const uint64_t n = a.n, n4 = n / 4;
+    const TvRange R = tv_range(n4, G, r);
     // the range as a bounded buffer: lanes past it read zeros (launch_tv keeps
     // every range below 2^28 float4)
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(src + R.lo * 4), 0, (uint32_t)(R.len * 16), 0x00020000);
+        const_cast<float *>(a.src + R.lo * 4), 0, (uint32_t)(R.len * 16), 0x00020000);
     const uint32_t steps = (uint32_t)((R.len + 63) / 64);  // 64 float4 per wave step
     const uint32_t mine = steps > wave ? (steps - wave + TNW - 1) / TNW : 0u;
     auto load = [&](uint32_t m) -> float4 {
@@ -115,11 +139,11 @@ __global__ void __launch_bounds__(TWG, 8) tv_scan(const float *__restrict__ src,
         }
     }
     // the ragged tail (n % 4 elements) closes the last range
-    if (w == G - 1 && tid == 0) {
+    if (r == G - 1 && tid == 0) {
         for (uint64_t e = n4 * 4; e < n; ++e) {
-            const float x = src[e], a = fabsf(x);
-            mx = max(mx, f2u(a));
-            if (a >= t) {
+            const float x = a.src[e], ax = fabsf(x);
+            mx = max(mx, f2u(ax));
+            if (ax >= t) {
                 const uint32_t o = atomicAdd(&s_n, 1u);
                 ++cnt;
                 if (o < LCAP) { s_pos[o] = (uint32_t)e; s_val[o] = x; }
@@ -131,68 +155,68 @@ __global__ void __launch_bounds__(TWG, 8) tv_scan(const float *__restrict__ src,
     if (lane == 0) { s_cnt[wave] = cnt; s_max[wave] = mx; }
     __syncthreads();
     const uint32_t listed = s_n;
-    if (tid == 0) {
-        uint32_t c = 0, m = 0;
-        for (uint32_t i = 0; i < TNW; ++i) { c += s_cnt[i]; m = max(m, s_max[i]); }
-        wg_cnt[w] = c;
-        wg_max[w] = m;
+    uint32_t c = 0;
+    for (uint32_t i = 0; i < TNW; ++i) c += s_cnt[i];
+    if (tid == 0) {  // publish: the maximum, then the tagged count
+        uint32_t m = 0;
+        for (uint32_t i = 0; i < TNW; ++i) m = max(m, s_max[i]);
+        st_sc1(&a.rmax[r], m);
+        __builtin_amdgcn_s_waitcnt(0);
+        st_sc1(&a.desc[r], ((uint64_t)a.tag << 32) | c);
     }
-    // position order: rank = listed entries with a smaller position
-    if (listed <= LCAP) {
-        for (uint32_t e = tid; e < listed; e += TWG) {
-            const uint32_t p = s_pos[e];
-            uint32_t r = 0;
-            for (uint32_t x = 0; x < listed; ++x) r += s_pos[x] < p;
-            stage_pos[(size_t)w * LCAP + r] = p;
-            stage_val[(size_t)w * LCAP + r] = s_val[e];
+    // look-back: the counts of ranges 0 .. r-1 (taken earlier, so held by
+    // running or finished workgroups), 64 per round trip by wave 0
+    if (wave == 0) {
+        uint64_t P = 0;
+        for (uint32_t i0 = 0; i0 < r; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            uint64_t d = i < r ? ld_sc1(&a.desc[i]) : 0ull;
+            bool pend = i < r && (uint32_t)(d >> 32) != a.tag;
+            // Stale ones: only the latest pending range (the likeliest to
+            // publish last) is polled, from one lane; then
+            // the rest are re-read once -- every lane of every waiting
+            // workgroup polling would flood the fabric the streaming loads use.
+            for (uint32_t spins = 0;; ++spins) {
+                const uint64_t pm = __ballot(pend);
+                if (!pm) break;
+                const uint32_t hl = 63u - (uint32_t)__clzll((long long)pm);
+                __builtin_amdgcn_s_sleep(8);
+                if (lane == hl) {
+                    d = ld_sc1(&a.desc[i]);
+                    pend = (uint32_t)(d >> 32) != a.tag;
+                }
+                if (!__ballot(lane == hl && pend) && pend) {
+                    d = ld_sc1(&a.desc[i]);
+                    pend = (uint32_t)(d >> 32) != a.tag;
+                }
+                if (spins > (1u << 20)) {  // ~0.5 s: give up; the count is poisoned below
+                    if (lane == 0) g_or(a.fail, FAIL_SPIN_TIMEOUT);
+                    break;
+                }
+            }
+            P += (uint32_t)d;
         }
+        P = wave_sum64(P);
+        if (lane == 0) s_P = P;
     }
-}
-
-struct TvFillArgs {
-    const float *src;
-    uint64_t n;
-    uint32_t k, cap;
-    uint32_t *idx;
-    float *val;
-    uint32_t *count_out;
-    KeyState *state;
-    const CallParams *cp;
-    const uint32_t *wg_cnt;
-    const uint32_t *wg_max;
-    const uint32_t *stage_pos;
-    const float *stage_val;
-};
-
-__global__ void __launch_bounds__(TWG) tv_fill(TvFillArgs a) {
-    __shared__ uint64_t sh64[TNW];
-    __shared__ uint32_t s_mx[TNW];
-    __shared__ uint32_t sh[TNW + 1];
-    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    const float t = a.cp->t;  // the state slot itself is rewritten by workgroup 0 below
-    uint64_t tot = 0, bef = 0;
-    uint32_t mx = 0;
-    for (uint32_t i = tid; i < G; i += TWG) {
-        const uint32_t c = a.wg_cnt[i];
-        tot += c;
-        if (i < w) bef += c;
-        mx = max(mx, a.wg_max[i]);
-    }
-    const uint64_t cnt = blk_sum64<TNW>(tot, sh64);
-    const uint64_t P = blk_sum64<TNW>(bef, sh64);
-    const uint32_t c = a.wg_cnt[w];
+    __syncthreads();
+    const uint64_t P = s_P;
     if (P < a.cap && c) {
         const uint32_t m = (uint32_t)std::min<uint64_t>(c, a.cap - P);
-        if (c <= LCAP) {
-            for (uint32_t i = tid; i < m; i += TWG) {
-                a.idx[P + i] = a.stage_pos[(size_t)w * LCAP + i];
-                a.val[P + i] = a.stage_val[(size_t)w * LCAP + i];
+        if (listed <= LCAP) {
+            // position order: rank = listed entries with a smaller position
+            for (uint32_t e = tid; e < listed; e += TWG) {
+                const uint32_t p = s_pos[e];
+                uint32_t rk = 0;
+                for (uint32_t x = 0; x < listed; ++x) rk += s_pos[x] < p;
+                if (rk < m) {
+                    a.idx[P + rk] = p;
+                    a.val[P + rk] = s_val[e];
+                }
             }
         } else {
             // the range's list overflowed: its qualifiers again, in order
-            const uint64_t n4 = a.n / 4;
-            const TvRange R = tv_range(n4, G, w);
-            const uint64_t units = R.len + (w == G - 1 && a.n % 4 ? 1u : 0u);  // + the ragged tail
+            const uint64_t units = R.len + (r == G - 1 && n % 4 ? 1u : 0u);  // + the ragged tail
             uint64_t base = 0;
             for (uint64_t f0 = 0; f0 < units && base < m; f0 += TWG) {
                 const uint64_t f = f0 + tid;
@@ -202,7 +226,7 @@ __global__ void __launch_bounds__(TWG) tv_fill(TvFillArgs a) {
 #pragma unroll
                     for (uint32_t j = 0; j < 4; ++j) {
                         const uint64_t e = (R.lo + f) * 4 + j;
-                        if (e < a.n) {
+                        if (e < n) {
                             xs[j] = a.src[e];
                             q |= (uint32_t)(fabsf(xs[j]) >= t) << j;
                         }
@@ -225,21 +249,26 @@ __global__ void __launch_bounds__(TWG) tv_fill(TvFillArgs a) {
             }
         }
     }
-    if (w == 0) {
-        mx = wave_max(mx);
-        if ((tid & 63) == 0) s_mx[tid >> 6] = mx;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t g = 0;
-            for (uint32_t i = 0; i < TNW; ++i) g = max(g, s_mx[i]);
-            const float gmax = a.n ? u2f(g) : -1.f;
-            float nt = t;
-            if ((uint64_t)a.k > cnt) nt = (float)((double)t * 0.99);
-            else if ((uint64_t)a.k < cnt) nt = (float)fma(0.01 * (double)cnt / (double)a.k, (double)gmax, (double)t);
-            a.state->t = nt;
-            a.state->init = 1;
-            *a.count_out = (uint32_t)std::min<uint64_t>(cnt, a.cap);
-        }
+    // the last range has seen every range's count (the look-back), and each
+    // range stored its maximum before its count: fold them
+    if (r != G - 1) return;
+    uint32_t gm = 0;
+    for (uint32_t i = tid; i < G; i += TWG) gm = max(gm, ld_sc1(&a.rmax[i]));
+    const uint64_t cntall = P + c;
+    gm = wave_max(gm);
+    if (lane == 0) s_max[wave] = gm;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t g = 0;
+        for (uint32_t i = 0; i < TNW; ++i) g = max(g, s_max[i]);
+        const float gmax = n ? u2f(g) : -1.f;
+        float nt = t;
+        if ((uint64_t)a.k > cntall) nt = (float)((double)t * 0.99);
+        else if ((uint64_t)a.k < cntall) nt = (float)fma(0.01 * (double)cntall / (double)a.k, (double)gmax, (double)t);
+        a.state->t = nt;
+        a.state->init = 1;
+        *a.count_out = (uint32_t)std::min<uint64_t>(cntall, a.cap);
+        if (ld_sc1(a.fail)) *a.count_out = POISON_COUNT;  // a bounded wait gave up: untrusted output
     }
 }
 
@@ -257,9 +286,7 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     const uint32_t G = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(2u * (uint64_t)a.num_cu, TV_MAXG), (n4 + 4095) / 4096));
     if (n4 / G + 1 >= (1ull << 28)) return hipErrorInvalidValue;  // a range must fit one buffer descriptor
-    if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    tv_scan<<<G, TWG, 0, s>>>(a.src, a.n, a.state, ws.tile_cnt, ws.tile_aux, ws.stage_pos, ws.stage_val, ws.cp);
-    TvFillArgs f;
+    TvArgs f;
     f.src = a.src;
     f.n = a.n;
     f.k = a.k;
@@ -268,13 +295,16 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     f.val = a.val;
     f.count_out = a.count_out;
     f.state = a.state;
-    f.cp = ws.cp;
-    f.wg_cnt = ws.tile_cnt;
-    f.wg_max = ws.tile_aux;
-    f.stage_pos = ws.stage_pos;
-    f.stage_val = ws.stage_val;
+    f.desc = reinterpret_cast<uint64_t *>(ws.tile_cnt);
+    f.rmax = ws.tile_aux;
+    f.tag = a.tag;
+    f.fail = ws.fail;
+    f.ticket = ws.tv_ticket;
+    f.base = a.ticket_base;
+    if (a.grid_out) *a.grid_out = G;
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    tv_pass<<<G, TWG, 0, s>>>(f);
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    tv_fill<<<G, TWG, 0, s>>>(f);
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
     return hipGetLastError();
 }

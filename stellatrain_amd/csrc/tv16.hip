@@ -308,7 +308,10 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
         uint32_t first = 1;
         if (flane() == 0) first = atomicAdd(&L.mid[j % CIDR], 1u);
         grab = uni(first) == 0;
-        if (grab && flane() == 0) nx = g_add(&C.cc()->next, 1u);
+        // a launch with no more chunks than workgroups hands every chunk out
+        // at slot 0 (each workgroup takes one as it starts): the counter has
+        // nothing left, so skip its round trip (and the traffic on its line)
+        if (grab && flane() == 0) nx = C.A.K <= C.G ? C.A.K : g_add(&C.cc()->next, 1u);
     };
     for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
         if (!tried && m0 >= mine / 2) try_take();

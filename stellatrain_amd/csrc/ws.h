@@ -85,6 +85,7 @@ struct DevWS {
     uint32_t *fail;      // sticky failure bits
     uint32_t *cand;      // regime-B window entries, CAND_WORDS per bucket of a launch
     uint32_t *misc;      // small scratch (counts)
+    uint64_t *tv_ticket;   // threshold-v: ranges taken, monotonic over the workspace's life
     float *sums;         // thresholdv16: one sum per 16-float line
     uint32_t *tile_cnt;  // per-tile qualifier counts
     uint32_t *tile_aux;  // per-tile secondary counts (threshold-v max, top-k ties)
@@ -153,6 +154,9 @@ struct TvLaunch {
     bool first;
     int num_cu;
     hipEvent_t *ev;
+    uint32_t tag;          // call tag (>= 1) of the range descriptors at ws.tile_cnt (2 words per range)
+    uint64_t ticket_base;  // ws.tv_ticket's value when this call starts
+    uint32_t *grid_out;    // receives the launch's range count (the ticket advances by it)
 };
 hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s);
 
