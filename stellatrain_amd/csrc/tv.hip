@@ -33,7 +33,10 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t TWG = 1024;       // threads per workgroup (16 waves)
 constexpr uint32_t TNW = TWG / 64;
-constexpr uint32_t SCAN_D = 4;       // float4 loads in flight per lane
+#ifndef STG_TV_SCAN_D
+#define STG_TV_SCAN_D 4
+#endif
+constexpr uint32_t SCAN_D = STG_TV_SCAN_D;  // float4 loads in flight per lane
 constexpr uint32_t LCAP = TV_SCAP;   // qualifiers listed in LDS per range
 
 __global__ void tv_init_state(KeyState *st, const RSel *rs) {

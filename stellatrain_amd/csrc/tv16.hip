@@ -88,6 +88,9 @@ constexpr uint32_t WL_B = STG_TV16_WL_B;  // window candidates listed in LDS per
 #ifndef STG_TV16_DIAG_NOEMIT
 #define STG_TV16_DIAG_NOEMIT 0
 #endif
+#ifndef STG_TV16_DIAG_STATIC0
+#define STG_TV16_DIAG_STATIC0 0
+#endif
 #ifndef STG_TV16_DIAG_STORES
 #define STG_TV16_DIAG_STORES 0
 #endif
@@ -677,7 +680,11 @@ tv16_batch(BatchArgs A) {
         // workgroup's slots therefore hold increasing chunks, chunks are taken
         // in order, and a chunk is only ever taken by a running workgroup: no
         // wait in this launch points at a workgroup that is not resident.
+#if STG_TV16_DIAG_STATIC0  // diagnostics only (co-residency dependent): slot 0 = workgroup id when K <= G
+        L.cid[0] = A.K <= C.G ? C.w : g_add(&C.cc()->next, 1u);
+#else
         L.cid[0] = g_add(&C.cc()->next, 1u);
+#endif
         for (uint32_t i = 0; i < CIDR; ++i) { L.cok[i] = 0; L.mid[i] = 0; }
         L.cok[0] = 1;
     }
