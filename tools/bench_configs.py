@@ -441,11 +441,12 @@ def main():
     import torch
     from stellatrain_amd import make_compressor
     only = set(a.only.split(","))
-    if "c2" in only:
-        for m in ("topk", "topk_exact"):
+    for m, tag in (("topk", "c2"), ("topk_exact", "c2")):
+        if tag in only or m in only:  # "topk" / "topk_exact": one mode alone (PMC passes)
             emit(time_device(torch, make_compressor(m), m, 64, 0.99, a.calls, 8, 9))
-    if "c3" in only:
+    if "c3" in only or "c3dev" in only:
         emit(time_device(torch, make_compressor("thresholdv"), "thresholdv", 256, 0.999, a.calls, 8, 3))
+    if "c3" in only:
         emit(host_inclusive(torch, "thresholdv", 256, 0.999, 12))
     if "e2e" in only:
         emit(host_inclusive(torch, "thresholdv16", 64, 0.99, 24))
