@@ -50,20 +50,19 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
     auto add = [&](uint32_t key) {
         if ((key & mask) == prefix) atomicAdd(&hc[(key >> SHIFT) & (NB - 1)], 1u);
     };
-    // UF float4 loads per thread in flight before any is used
+    // UF float4 loads per thread per step, double-buffered: the next step's
+    // loads are issued before this step's keys are counted, so 2 x UF x 16 B
+    // per thread stay in flight (128 KiB per CU; one step's worth, 64 KiB, is
+    // under what hides an HBM miss)
     constexpr uint32_t UF = 4;
-    for (size_t i0 = (size_t)blockIdx.x * HWG + threadIdx.x; i0 < m4; i0 += UF * stride) {
-        float4 v[UF];
-        if (i0 + (UF - 1) * stride < m4) {  // all UF loads in range: issue them together
+    // unconditional loads (a clamped index past the end; those keys are not
+    // counted): a load under a branch makes the compiler wait for every load
+    // at the join
+    auto load_step = [&](size_t i0, float4 (&v)[UF]) {
 #pragma unroll
-            for (uint32_t u = 0; u < UF; ++u) v[u] = a4[i0 + u * stride];
-        } else {
-#pragma unroll
-            for (uint32_t u = 0; u < UF; ++u) {
-                const size_t i = i0 + u * stride;
-                v[u] = i < m4 ? a4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
+        for (uint32_t u = 0; u < UF; ++u) v[u] = a4[std::min(i0 + u * stride, m4 - 1)];
+    };
+    auto count_step = [&](size_t i0, const float4 (&v)[UF]) {
 #pragma unroll
         for (uint32_t u = 0; u < UF; ++u) {
             const size_t i = i0 + u * stride;
@@ -72,6 +71,20 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
             uint32_t k2 = f2u(v[u].z) & 0x7fffffffu, k3 = f2u(v[u].w) & 0x7fffffffu;
             if (4 * i + 3 == m - 1) k3 &= last_mask;
             add(k0); add(k1); add(k2); add(k3);
+        }
+    };
+    // ping-pong over two register sets (no copies between them, so counting
+    // one set waits only for its own loads)
+    const size_t step = UF * stride;
+    size_t i0 = (size_t)blockIdx.x * HWG + threadIdx.x;
+    float4 va[UF], vb[UF];
+    if (m4) {
+        load_step(i0, va);
+        for (; i0 < m4; i0 += 2 * step) {
+            load_step(i0 + step, vb);
+            count_step(i0, va);
+            load_step(i0 + 2 * step, va);
+            count_step(i0 + step, vb);
         }
     }
     if (blockIdx.x == 0) {

@@ -283,6 +283,7 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
             for (uint32_t r = 0; r < 4; ++r) {
                 if ((qw >> r) & 1u) {
                     const uint64_t slot = win_before + wr++;
+                    if (slot >= a.k) continue;  // never with a consistent select; keeps a bad one in bounds
                     a.idx[slot] = a.bug_compat ? (uint32_t)slot : x[r].x + (uint32_t)a.idx_offset;
                     a.val[slot] = u2f(x[r].y);
                 }
@@ -321,6 +322,7 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
                     const uint32_t b = u * 4 + j;
                     if ((qw >> b) & 1u) {
                         const uint64_t slot = win_before + sw[b];
+                        if (slot >= a.k) continue;  // never with a consistent select; keeps a bad one in bounds
                         a.idx[slot] = a.bug_compat ? (uint32_t)slot : (uint32_t)(e + j) + (uint32_t)a.idx_offset;
                         a.val[slot] = comp(v[u], j);
                     }
