@@ -507,7 +507,8 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         const size_t ntiles = (n + stg::TV_TILE - 1) / stg::TV_TILE;
         // superset entries (two words each, stg::TOPK_SUP_CAP per tile); per-tile
         // counts, their prefixes and the superset counts
-        if ((rc = ws->ensure(2 * ntiles * stg::TOPK_SUP_CAP, 3 * ntiles + 1, 1))) return rc;
+        // + the level-2 bin's list (two words per key)
+        if ((rc = ws->ensure(2 * ntiles * stg::TOPK_SUP_CAP + 2 * stg::TOPK_LIST_CAP, 3 * ntiles + 1, 1))) return rc;
         stg::TopkLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, h->method == M_TOPK, d_count,
                           h->num_cu, ev};
         HIP_TRY(stg::launch_topk(a, ws->d, s));

@@ -22,7 +22,7 @@ __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
     constexpr uint32_t NB = 1u << NBITS;
     constexpr uint32_t PER = (NB + NT - 1) / NT;
     __shared__ uint32_t wsum[NT / 64];
-    __shared__ uint32_t s_bin, s_before;
+    __shared__ uint32_t s_bin, s_before, s_cnt;
     const uint32_t t = threadIdx.x, lane = __lane_id(), wave = t >> 6;
     const uint32_t prefix = FIRST ? 0u : ld_sc1(&st->prefix);
     const uint32_t rank = FIRST ? rank_arg : ld_sc1(&st->rank);
@@ -50,7 +50,7 @@ __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
         uint32_t acc = before;
 #pragma unroll
         for (uint32_t j = 0; j < PER; ++j) {
-            if (rank - acc < c[j]) { s_bin = NB - 1 - (PER * t + j); s_before = acc; break; }
+            if (rank - acc < c[j]) { s_bin = NB - 1 - (PER * t + j); s_before = acc; s_cnt = c[j]; break; }
             acc += c[j];
         }
     }
@@ -67,6 +67,7 @@ __device__ void pick_level(RSel *st, uint64_t extra_zeros, uint32_t rank_arg) {
         const uint32_t b = hit ? s_bin : 0u;  // rank out of range: degenerate
         const uint32_t bb = hit ? s_before : 0u;
         st_sc1(&st->rank, rank - bb);
+        st_sc1(&st->pad[1], hit ? s_cnt : 0u);  // the chosen bin's keys (top-k's level-2 list)
         st_sc1(&st->cnt_gt, (FIRST ? 0u : ld_sc1(&st->cnt_gt)) + bb);
         st_sc1(&st->prefix, prefix | (b << SHIFT));
         st_sc1(&st->mask, (FIRST ? 0u : ld_sc1(&st->mask)) | ((NB - 1) << SHIFT));

@@ -14,14 +14,21 @@
 // index order.  compress() returns the capacity (topk.cpp:25) and throws when
 // capacity < k (topk.cpp:33-34).
 //
-// GPU structure: two passes over the bucket, the rest over a 3 % superset:
+// GPU structure: two passes over the bucket, the rest over a ~3 % superset:
 //   rs_hist level 1 (select.hip; its last workgroup picks): the top 11 bits
 //     of the k-th magnitude T;
 //   tk_pass: every element at or above that bin goes, in index order, to its
 //     tile's superset region (an overflowing tile keeps only a count and is
 //     re-read later); the bin's elements fill the level-2 histogram;
-//   tk_pick level 2, tk_hist3 + tk_pick level 3 over the supersets: T exactly;
-//   tk_count2 + tk_scan: per-tile (> T, == T) counts and their prefixes;
+//   tk_pick level 2: bits 19..9 of T (and how many keys share that bin);
+//   buckets of <= TOPK_LIST_TILES tiles: tk_resolve lists the keys of T's
+//     level-2 bin (~100 at 64 MiB) and counts each tile's keys above it;
+//     tk_final (one workgroup) takes T from the list, fixes the per-tile
+//     (> T, == T) counts and scans them.  A bin holding more keys than the
+//     list (ties) falls back inside the same two launches: tk_resolve fills
+//     the level-3 histogram and tk_final picks T and recounts the bin's keys
+//     per tile itself (slow, ties only);
+//   larger buckets: tk_hist3 + tk_pick level 3, tk_count2 + tk_scan;
 //   tk_emit2: the ordered emission from the supersets.
 #include <algorithm>
 
@@ -88,7 +95,10 @@ __global__ void __launch_bounds__(STG_WG) tk_pass(const float *__restrict__ a, s
     __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
     for (uint32_t i = threadIdx.x; i < NB2; i += STG_WG) h2[i] = 0;
     const uint32_t lo = rs->prefix;  // level 1: bits 30..20 of T, the rest 0
-    if (blockIdx.x == 0 && threadIdx.x == 0) rs->pad[0] = lo;  // for the later passes (nothing else uses pad)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        rs->pad[0] = lo;  // for the later passes
+        rs->pad[2] = 0;   // the level-2 bin's list (tk_resolve)
+    }
     __syncthreads();
     const uint32_t tile = blockIdx.x, lane = __lane_id(), wave = threadIdx.x >> 6;
     const size_t base = (size_t)tile * TV_TILE;
@@ -225,6 +235,187 @@ __global__ void __launch_bounds__(STG_WG) tk_count2(const float *__restrict__ a,
         for (uint32_t w = 0; w < STG_WAVES; ++w) { g += s_c[w]; e += s_c[STG_WAVES + w]; }
         tile_gt[blockIdx.x] = g;
         tile_eq[blockIdx.x] = e;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Level 3 without a histogram pass (buckets of <= TOPK_LIST_TILES tiles): T's
+// level-2 bin spans 2^9 ulps and holds ~100 keys at 64 MiB, so they are listed
+// and one workgroup finishes the select, the per-tile counts and their scan.
+// ---------------------------------------------------------------------------
+struct TkList {
+    uint2 *list;       // {element, key} of the level-2 bin's keys, TOPK_LIST_CAP
+    uint32_t ntiles;
+    uint64_t zeros;    // implicit +0.0 keys (bug-compat)
+};
+
+// Per tile: the superset's keys above T's level-2 bin (count) and those in it
+// (listed); with a crowded bin (ties: more than the list holds) the level-3
+// histogram instead.
+template <bool VEC>
+__global__ void __launch_bounds__(STG_WG) tk_resolve(const float *__restrict__ a, size_t m, uint32_t last_mask,
+                                                     RSel *__restrict__ rs, const uint2 *__restrict__ sup,
+                                                     const uint32_t *__restrict__ sup_n, uint32_t *__restrict__ tile_gt,
+                                                     TkList L) {
+    __shared__ uint32_t h3[512];
+    __shared__ uint2 s_list[TOPK_LIST_CAP];  // this tile's keys in the bin, then one global append
+    __shared__ uint32_t s_c[STG_WAVES], s_ln, s_base;
+    const uint32_t prefix = rs->prefix, mask = rs->mask, lo = rs->pad[0];  // bits 30..9 of T
+    const uint32_t real = rs->pad[1] - (prefix == 0 ? (uint32_t)L.zeros : 0u);  // listed keys
+    const bool listed = real <= TOPK_LIST_CAP;
+    if (threadIdx.x == 0) s_ln = 0;
+    if (!listed)
+        for (uint32_t i = threadIdx.x; i < 512; i += STG_WG) h3[i] = 0;
+    __syncthreads();
+    uint32_t above = 0;
+    for_tile<VEC>(a, m, last_mask, lo, sup, sup_n[blockIdx.x], [&](uint32_t e, uint32_t bits) {
+        const uint32_t key = mag(bits), top = key & mask;
+        above += top > prefix;
+        if (top == prefix) {
+            if (listed) {
+                const uint32_t j = atomicAdd(&s_ln, 1u);
+                if (j < TOPK_LIST_CAP) s_list[j] = make_uint2(e, key);
+            } else {
+                atomicAdd(&h3[key & 511u], 1u);
+            }
+        }
+    });
+    above = wave_sum(above);
+    if (__lane_id() == 0) s_c[threadIdx.x >> 6] = above;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t g = 0;
+        for (uint32_t w = 0; w < STG_WAVES; ++w) g += s_c[w];
+        tile_gt[blockIdx.x] = g;
+        // one device atomic per tile with keys in the bin (a word takes ~90 per us)
+        s_base = s_ln ? g_add(&rs->pad[2], s_ln) : 0u;
+    }
+    __syncthreads();
+    if (listed) {
+        const uint32_t n = std::min(s_ln, TOPK_LIST_CAP);
+        for (uint32_t i = threadIdx.x; i < n; i += STG_WG)
+            if (s_base + i < TOPK_LIST_CAP) L.list[s_base + i] = s_list[i];
+    }
+    if (!listed)
+        for (uint32_t i = threadIdx.x; i < 512; i += STG_WG)
+            if (h3[i]) g_add(&rs->hist[blockIdx.x % RS_SHARDS][i], h3[i]);
+}
+
+constexpr uint32_t FWGT = 1024;  // tk_final: one workgroup
+constexpr uint32_t FNWT = FWGT / 64;
+
+// One workgroup: T from the list (or the level-3 histogram), the per-tile
+// (> T, == T) counts and their exclusive prefixes -- what tk_count2 + tk_scan
+// leave for the emission.
+template <bool VEC>
+__global__ void __launch_bounds__(FWGT) tk_final(const float *__restrict__ a, size_t m, uint32_t last_mask,
+                                                 RSel *__restrict__ rs, const uint2 *__restrict__ sup,
+                                                 const uint32_t *__restrict__ sup_n, uint32_t *__restrict__ tile_gt,
+                                                 uint32_t *__restrict__ tile_eq, TkList L) {
+    __shared__ uint32_t g[TOPK_LIST_TILES], q[TOPK_LIST_TILES];
+    __shared__ uint32_t h[512];
+    __shared__ uint32_t sh[FNWT + 1];
+    __shared__ uint32_t s_T, s_above;
+    const uint32_t tid = threadIdx.x, nt = L.ntiles;
+    const uint32_t prefix = rs->prefix, lo = rs->pad[0];
+    const uint32_t rank = rs->rank, cnt_gt = rs->cnt_gt;
+    const uint32_t real = rs->pad[1] - (prefix == 0 ? (uint32_t)L.zeros : 0u);
+    const bool listed = real <= TOPK_LIST_CAP;
+    const uint32_t nl = listed ? std::min(rs->pad[2], TOPK_LIST_CAP) : 0u;
+    for (uint32_t i = tid; i < 512; i += FWGT) h[i] = 0;
+    for (uint32_t t = tid; t < nt; t += FWGT) { g[t] = tile_gt[t]; q[t] = 0; }
+    __syncthreads();
+    uint32_t T;
+    if (listed) {
+        // the low 9 bits of the listed keys (+ the implicit zeros in the bin of 0)
+        for (uint32_t i = tid; i < nl; i += FWGT) atomicAdd(&h[L.list[i].y & 511u], 1u);
+        if (tid == 0 && prefix == 0 && L.zeros) atomicAdd(&h[0], (uint32_t)L.zeros);
+        __syncthreads();
+        {   // the bin of descending rank `rank`: thread i holds bin 511 - i, a
+            // workgroup scan gives the keys above it (a serial walk over 512 LDS
+            // words cost ~15 us)
+            const uint32_t c = tid < 512 ? h[511 - tid] : 0u;
+            uint32_t tot;
+            const uint32_t above = blk_excl_scan<FNWT>(c, sh, &tot);
+            if (tid < 512 && c && rank >= above && rank - above < c) {
+                s_T = prefix | (511u - tid);
+                s_above = above;
+            }
+            if (tid == 0 && rank >= tot) { s_T = prefix; s_above = tot; }  // rank out of range: degenerate
+        }
+        __syncthreads();
+        T = s_T;
+        for (uint32_t i = tid; i < nl; i += FWGT) {  // the listed keys' tiles
+            const uint2 x = L.list[i];
+            const uint32_t t = x.x / TV_TILE;
+            if (x.y > T) atomicAdd(&g[t], 1u);
+            else if (x.y == T) atomicAdd(&q[t], 1u);
+        }
+    } else {
+        // a crowded bin: tk_resolve filled the level-3 histogram; then every
+        // tile's keys in the bin again (slow, one workgroup; ties only)
+        pick_level<0, 9, FWGT, RS_SHARDS>(rs, L.zeros, 0);
+        if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // its stores done before the others read them
+        __syncthreads();
+        T = ld_sc1(&rs->prefix);
+        const uint32_t mask2 = 0x7ffffe00u;
+        for (uint32_t t = 0; t < nt; ++t) {
+            uint32_t cg = 0, ce = 0;
+            const uint32_t n = sup_n[t];
+            if (n <= SUP_CAP) {
+                for (uint32_t j = tid; j < n; j += FWGT) {
+                    const uint32_t key = mag(sup[(size_t)t * SUP_CAP + j].y);
+                    if ((key & mask2) == prefix) { cg += key > T; ce += key == T; }
+                }
+            } else {
+                const size_t base = (size_t)t * TV_TILE, end = std::min<size_t>(m, base + TV_TILE);
+                for (size_t e = base + tid; e < end; e += FWGT) {
+                    uint32_t key = mag(f2u(a[e]));
+                    if (e == m - 1) key &= last_mask;
+                    if (key >= lo && (key & mask2) == prefix) { cg += key > T; ce += key == T; }
+                }
+            }
+            cg = wave_sum(cg);
+            ce = wave_sum(ce);
+            if (__lane_id() == 0) { if (cg) atomicAdd(&g[t], cg); if (ce) atomicAdd(&q[t], ce); }
+        }
+        if (tid == 0) s_above = ld_sc1(&rs->cnt_gt) - cnt_gt;
+    }
+    __syncthreads();
+    // exclusive prefixes over the tiles, 8 consecutive tiles per thread
+    uint32_t cg = 0, ce = 0;
+    constexpr uint32_t PT8 = 8;
+    for (uint32_t t0 = 0; t0 < nt; t0 += PT8 * FWGT) {
+        const uint32_t tb = t0 + PT8 * tid;
+        uint32_t sg = 0, sq = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < PT8; ++i)
+            if (tb + i < nt) { sg += g[tb + i]; sq += q[tb + i]; }
+        uint32_t tg, tq;
+        uint32_t pg = cg + blk_excl_scan<FNWT>(sg, sh, &tg);
+        uint32_t pq = ce + blk_excl_scan<FNWT>(sq, sh, &tq);
+#pragma unroll
+        for (uint32_t i = 0; i < PT8; ++i) {
+            if (tb + i < nt) {
+                tile_gt[tb + i] = g[tb + i];
+                tile_eq[tb + i] = q[tb + i];
+                tile_gt[nt + tb + i] = pg;
+                tile_eq[nt + tb + i] = pq;
+                pg += g[tb + i];
+                pq += q[tb + i];
+            }
+        }
+        cg += tg;
+        ce += tq;
+    }
+    if (tid == 0) {
+        tile_gt[2 * nt] = cg;
+        tile_eq[2 * nt] = ce;
+        if (listed) {  // the select's result, as the histogram levels leave it
+            rs->prefix = T;
+            rs->cnt_gt = cnt_gt + s_above;
+            rs->rank = rank - s_above;
+        }
     }
 }
 
@@ -370,12 +561,20 @@ hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s) {
     if (vec) tk_pass<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
     else tk_pass<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
     tk_pick<9, 11><<<1, 1024, 0, s>>>(ws.rsel, zeros);
-    if (vec) tk_hist3<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
-    else tk_hist3<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
-    tk_pick<0, 9><<<1, 1024, 0, s>>>(ws.rsel, zeros);
-    if (vec) tk_count2<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux);
-    else tk_count2<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux);
-    tk_scan<<<1, STG_WG, 0, s>>>(ws.tile_cnt, ws.tile_aux, ntiles);
+    if (ntiles <= TOPK_LIST_TILES) {  // level 3 from the level-2 bin's list: two launches
+        TkList L{reinterpret_cast<uint2 *>(ws.sums) + (size_t)ntiles * SUP_CAP, ntiles, zeros};
+        if (vec) tk_resolve<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, L);
+        else tk_resolve<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, L);
+        if (vec) tk_final<true><<<1, FWGT, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux, L);
+        else tk_final<false><<<1, FWGT, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux, L);
+    } else {
+        if (vec) tk_hist3<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
+        else tk_hist3<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n);
+        tk_pick<0, 9><<<1, 1024, 0, s>>>(ws.rsel, zeros);
+        if (vec) tk_count2<true><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux);
+        else tk_count2<false><<<ntiles, STG_WG, 0, s>>>(a.src, m, last_mask, ws.rsel, sup, sup_n, ws.tile_cnt, ws.tile_aux);
+        tk_scan<<<1, STG_WG, 0, s>>>(ws.tile_cnt, ws.tile_aux, ntiles);
+    }
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
     TkArgs t;
     t.a = a.src;

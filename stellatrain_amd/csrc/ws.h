@@ -15,6 +15,8 @@ constexpr uint32_t TV16_SCAN_LDS = 35584;     // LDS bytes of a scan workgroup (
 
 constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)
 constexpr uint32_t TOPK_SUP_CAP = 1024;      // top-k superset entries kept per tile
+constexpr uint32_t TOPK_LIST_CAP = 4096;     // top-k: keys of T's level-2 bin listed for the final select
+constexpr uint32_t TOPK_LIST_TILES = 8192;   // ... when the bucket has at most this many tiles (64 Mi floats)
 constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
 constexpr uint32_t TV_SCAP = 2048;           // threshold-v qualifiers listed per range
 
@@ -68,7 +70,7 @@ struct RSel {
     uint32_t rank;      // remaining rank (0-based, descending) inside the prefix
     uint32_t cnt_gt;    // keys strictly above the prefix range
     uint32_t done;      // classes of workgroups done with the current pass (the last one picks)
-    uint32_t pad[3];    // pad[0]: top-k's superset floor
+    uint32_t pad[3];    // pad[0]: top-k's superset floor; [1]: keys in the last picked bin; [2]: top-k list length
     uint32_t done64[64];  // workgroups done, per class blockIdx.x % 64
     // The level histogram in RS_SHARDS copies, summed by the pick: device-scope
     // atomics on one word serialise at the memory side (~90 per us), so a

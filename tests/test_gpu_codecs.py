@@ -182,6 +182,44 @@ def test_topk_exact(gpu, oracle, n, k, off):
     assert_same_stream(idx.cpu().numpy().view(np.uint32), val.cpu().numpy(), io, vo, k)
 
 
+def _quantized(n, seed, step):
+    """D1 values rounded to multiples of `step`: few distinct magnitudes, so the
+    k-th magnitude is tied many times over."""
+    x = synth(n, seed).astype(np.float64)
+    return (np.round(x / step) * step).astype(np.float32)
+
+
+# Ties at T: (a) ~1.3k equal keys in T's level-2 bin (the listed select);
+# (b) ~26k equal keys (more than the list holds: the level-3 histogram and the
+# one-workgroup recount); (c) 90 % zeros with k past the nonzeros (T = 0, every
+# tile past its superset capacity).
+@pytest.mark.parametrize("case", ["ties_listed", "ties_crowded", "zeros_t0"])
+@pytest.mark.parametrize("bug_compat", [False, True])
+def test_topk_ties(gpu, oracle, case, bug_compat):
+    import torch
+    from stellatrain_amd import TopkCompressor
+    n = 1 << 20
+    if case == "ties_listed":
+        src, k = _quantized(n, seed_for(13, 0), 5e-6), 10485
+    elif case == "ties_crowded":
+        src, k = _quantized(n, seed_for(13, 1), 1e-4), 10485
+    else:
+        src, k = synth(n, seed_for(13, 2), D3, 9000), 200000
+    if bug_compat:
+        k = min(k, n // 8) if case != "zeros_t0" else n // 4 + 5000  # past the copied floats: T = 0
+    co, io, vo = oracle.topk_compress(src, k, bug_compat=bug_compat)
+    comp = TopkCompressor(exact=not bug_compat)
+    idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+    val = torch.zeros(k, dtype=torch.float32, device=gpu)
+    assert comp.compress("x", torch.from_numpy(src).to(gpu), k, idx, val) == co
+    if bug_compat:
+        np.testing.assert_array_equal(idx.cpu().numpy(), np.arange(k))
+        assert_topk_values(val.cpu().numpy(), vo)
+    else:
+        assert_same_stream(idx.cpu().numpy().view(np.uint32), val.cpu().numpy(), io, vo, k)
+    comp.check_device()
+
+
 def test_topk_capacity_error(gpu):
     import torch
     from stellatrain_amd import CodecError, TopkCompressor
