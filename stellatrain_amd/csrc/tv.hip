@@ -10,8 +10,8 @@
 // k < cnt -> t = fma(0.01*cnt/k, gmax, t) in double (GCC contracts it at -O3).
 // Returns min(cnt, cap).  The state is keyed by the src pointer (:44).
 //
-// GPU structure: one launch, HBM-bound (tv_pass).  1024-thread workgroups (2
-// per CU) take contiguous ranges of the bucket in ticket order; 16 waves
+// GPU structure: one launch, HBM-bound (tv_pass).  1024-thread workgroups
+// (STG_TV_WPC per CU) take contiguous ranges of the bucket in ticket order; 16 waves
 // stream the range with a rolling pipeline of SCAN_D nontemporal float4 loads
 // per lane, count the qualifiers and max|x|, and list the qualifiers
 // (position, value) in LDS; the range publishes its count, sums the counts of
@@ -33,8 +33,11 @@ typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t TWG = 1024;       // threads per workgroup (16 waves)
 constexpr uint32_t TNW = TWG / 64;
+#ifndef STG_TV_WPC
+#define STG_TV_WPC 1  // workgroups per CU (1 with 6 loads in flight per lane: 52.3 us at C3; 2 with 4: 55.6)
+#endif
 #ifndef STG_TV_SCAN_D
-#define STG_TV_SCAN_D 4
+#define STG_TV_SCAN_D 6
 #endif
 constexpr uint32_t SCAN_D = STG_TV_SCAN_D;  // float4 loads in flight per lane
 constexpr uint32_t LCAP = TV_SCAP;   // qualifiers listed in LDS per range
@@ -284,10 +287,10 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
         if (e != hipSuccess) return e;
         tv_init_state<<<1, 1, 0, s>>>(a.state, ws.rsel);
     }
-    // 2 workgroups per CU, each with >= 64 KiB of the bucket
+    // STG_TV_WPC workgroups per CU, each with >= 64 KiB of the bucket
     const uint64_t n4 = a.n / 4;
     const uint32_t G = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>(std::min<uint64_t>(2u * (uint64_t)a.num_cu, TV_MAXG), (n4 + 4095) / 4096));
+        1, std::min<uint64_t>(std::min<uint64_t>((uint64_t)STG_TV_WPC * a.num_cu, TV_MAXG), (n4 + 4095) / 4096));
     if (n4 / G + 1 >= (1ull << 28)) return hipErrorInvalidValue;  // a range must fit one buffer descriptor
     TvArgs f;
     f.src = a.src;
