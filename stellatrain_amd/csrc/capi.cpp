@@ -24,6 +24,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../../include/stg/codec.h"
 #include "ws.h"
 
@@ -591,14 +593,37 @@ int stg_codec_destroy(stg_codec_t h) {
 
 const char *stg_codec_name(stg_codec_t h) { return h ? h->name.c_str() : ""; }
 
+namespace {
+// The reference times each compress task as "CRIT_PATH_compress"
+// (engine/modules/compress.cpp:140-142, record_stat_start/end).  With
+// STG_ROCTX=1 every compress entry point is a roctx range of that name, so
+// `rocprofv3 --marker-trace --kernel-trace` shows the host side of each call
+// next to its kernels.
+struct CritPath {
+    bool on;
+    CritPath() : on(enabled()) {
+        if (on) roctxRangePushA("CRIT_PATH_compress");
+    }
+    ~CritPath() {
+        if (on) roctxRangePop();
+    }
+    static bool enabled() {
+        static const bool v = getenv("STG_ROCTX") && atoi(getenv("STG_ROCTX")) == 1;
+        return v;
+    }
+};
+}  // namespace
+
 int stg_codec_compress_device(stg_codec_t h, const char *key, const float *d_src, size_t n, uint32_t k,
                               uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset,
                               uint32_t *d_count, void *stream) {
+    CritPath crit_path;
     return run_device(h, key, d_src, d_src, n, k, d_idx, idx_cap, d_val, val_cap, idx_offset, d_count,
                       static_cast<hipStream_t>(stream));
 }
 
 int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, size_t nbuckets, void *stream) {
+    CritPath crit_path;
     if (!h) return fail(STG_ERR_INVALID, "null codec handle");
     if (nbuckets && !buckets) return fail(STG_ERR_INVALID, "null bucket array");
     for (size_t i = 0; i < nbuckets; ++i) {
@@ -619,6 +644,7 @@ int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
 
 int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, float *const *d_residuals,
                                     size_t nbuckets, void *stream) {
+    CritPath crit_path;
     if (!h) return fail(STG_ERR_INVALID, "null codec handle");
     if (nbuckets && (!buckets || !d_residuals)) return fail(STG_ERR_INVALID, "null bucket or residual array");
     for (size_t i = 0; i < nbuckets; ++i) {
@@ -649,6 +675,7 @@ int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
 int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, size_t n, uint32_t k,
                             uint32_t *dst_idx, size_t idx_cap, float *dst_val, size_t val_cap, int32_t idx_offset,
                             size_t *out_count) {
+    CritPath crit_path;
     if (!h || !out_count) return fail(STG_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t s;
