@@ -156,18 +156,42 @@ __global__ void __launch_bounds__(STG_WG) mark_emit(uint8_t *__restrict__ mark, 
     if (w == 0 && tid == 0) *out_count = (uint32_t)total;
 }
 
+constexpr uint32_t WPER = MARK_TILE / STG_WG;  // 16 consecutive pairs per lane
+static_assert(WPER == 16, "four uint4 of indices per lane");
+
+// The lane's 16 pairs e .. e+15: their indices, and which of them win (bit b).
+// Every load is issued before any is used -- the 16 index loads together,
+// then the 16 winner words (clamped addresses, results masked) -- two round
+// trips per lane instead of 32 dependent ones.
+__device__ __forceinline__ uint32_t win_keep(const uint32_t *__restrict__ idx, size_t m, size_t n,
+                                             const uint32_t *__restrict__ win, size_t e, uint32_t (&j)[WPER]) {
+    if (e + WPER <= m && (reinterpret_cast<uintptr_t>(idx + e) & 15u) == 0) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(idx + e);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint4 v = p[q];
+            j[4 * q] = v.x; j[4 * q + 1] = v.y; j[4 * q + 2] = v.z; j[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t b = 0; b < WPER; ++b) j[b] = idx[std::min<size_t>(e + b, m - 1)];
+    }
+    uint32_t w[WPER];
+#pragma unroll
+    for (uint32_t b = 0; b < WPER; ++b) w[b] = win[j[b] < n ? j[b] : 0u];
+    uint32_t keep = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < WPER; ++b)
+        if (e + b < m && j[b] < n && w[b] == (uint32_t)(e + b) + 1u) keep |= 1u << b;
+    return keep;
+}
+
 __global__ void __launch_bounds__(STG_WG) win_count(const uint32_t *__restrict__ idx, size_t m, size_t n,
                                                     const uint32_t *__restrict__ win, uint32_t *__restrict__ tile_cnt) {
     __shared__ uint32_t s[STG_WAVES];
-    const size_t e0 = (size_t)blockIdx.x * MARK_TILE;
-    uint32_t c = 0;
-    for (uint32_t b = threadIdx.x; b < MARK_TILE; b += STG_WG) {
-        const size_t i = e0 + b;
-        if (i < m) {
-            const uint32_t j = idx[i];
-            c += j < n && win[j] == (uint32_t)i + 1u;
-        }
-    }
+    const size_t e = (size_t)blockIdx.x * MARK_TILE + (size_t)WPER * threadIdx.x;
+    uint32_t j[WPER];
+    uint32_t c = e < m ? (uint32_t)__popc(win_keep(idx, m, n, win, e, j)) : 0u;
     c = wave_sum(c);
     if (__lane_id() == 0) s[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -196,25 +220,30 @@ __global__ void __launch_bounds__(STG_WG) win_emit1(const uint32_t *__restrict__
     }
     const uint64_t total = wg_sum64(tot, sh64);
     uint64_t P = wg_sum64(bef, sh64);
-    constexpr uint32_t PER = MARK_TILE / STG_WG;  // 16 consecutive pairs per lane
     for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-        const size_t e = (size_t)tile * MARK_TILE + (size_t)PER * tid;
-        uint32_t keep = 0;  // bit b: pair e + b wins
-        for (uint32_t b = 0; b < PER; ++b) {
-            const size_t i = e + b;
-            if (i < m) {
-                const uint32_t j = idx[i];
-                if (j < n && win[j] == (uint32_t)i + 1u) keep |= 1u << b;
+        const size_t e = (size_t)tile * MARK_TILE + (size_t)WPER * tid;
+        uint32_t j[WPER];
+        const uint32_t keep = e < m ? win_keep(idx, m, n, win, e, j) : 0u;
+        float v[WPER];  // the values, loaded alongside (clamped addresses)
+        if (e + WPER <= m && (reinterpret_cast<uintptr_t>(val + e) & 15u) == 0) {
+            const float4 *p = reinterpret_cast<const float4 *>(val + e);
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const float4 x = p[q];
+                v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
             }
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < WPER; ++b) v[b] = m ? val[std::min<size_t>(e + b, m - 1)] : 0.f;
         }
         uint32_t tc;
         uint32_t r = wg_excl_scan((uint32_t)__popc(keep), sh, &tc);
-        for (uint32_t b = 0; b < PER; ++b) {
+#pragma unroll
+        for (uint32_t b = 0; b < WPER; ++b) {
             if (keep >> b & 1u) {
-                const uint32_t j = idx[e + b];
-                out_idx[P + r] = j;
-                out_val[P + r] = (0.0f + val[e + b]) / 1.0f;
-                win[j] = 0;  // scratch back to zero for the next call
+                out_idx[P + r] = j[b];
+                out_val[P + r] = (0.0f + v[b]) / 1.0f;
+                win[j[b]] = 0;  // scratch back to zero for the next call
                 ++r;
             }
         }
