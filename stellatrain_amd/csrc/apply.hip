@@ -252,6 +252,85 @@ __global__ void __launch_bounds__(STG_WG) win_emit1(const uint32_t *__restrict__
     if (w == 0 && tid == 0) *out_count = (uint32_t)total;
 }
 
+// world == 1 in one launch after win_mark: tiles in ticket order (a workgroup
+// only waits on tiles taken before its own, so no co-residency is needed);
+// each publishes its winner count as a tagged word, sums the earlier tiles'
+// counts (look-back) and writes its winners at that offset; the last tile
+// writes the count.
+struct Win1Args {
+    const uint32_t *idx;
+    const float *val;
+    size_t m, n;
+    uint32_t ntiles;
+    uint32_t *win;
+    uint64_t *desc;     // per tile: {call tag:32 | winners:32}
+    uint64_t *ticket;   // tiles taken, monotonic over the scratch's calls (zero at creation)
+    uint64_t base;      // its value when this call starts
+    uint32_t tag;       // this call's tag, >= 1
+    uint32_t *out_idx;
+    float *out_val;
+    uint32_t *out_count;
+};
+
+__global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
+    __shared__ uint32_t sh[STG_WAVES + 1];
+    __shared__ uint32_t s_tile, s_bad;
+    __shared__ uint64_t s_P;
+    const uint32_t tid = threadIdx.x, lane = __lane_id();
+    if (tid == 0) { s_tile = (uint32_t)(g_add(a.ticket, 1ull) - a.base); s_bad = 0; }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const size_t e = (size_t)tile * MARK_TILE + (size_t)WPER * tid;
+    uint32_t j[WPER];
+    const uint32_t keep = e < a.m ? win_keep(a.idx, a.m, a.n, a.win, e, j) : 0u;
+    float v[WPER];
+    if (e + WPER <= a.m && (reinterpret_cast<uintptr_t>(a.val + e) & 15u) == 0) {
+        const float4 *p = reinterpret_cast<const float4 *>(a.val + e);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const float4 x = p[q];
+            v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t b = 0; b < WPER; ++b) v[b] = a.m ? a.val[std::min<size_t>(e + b, a.m - 1)] : 0.f;
+    }
+    uint32_t tc;
+    uint32_t r = wg_excl_scan((uint32_t)__popc(keep), sh, &tc);
+    if (tid == 0) st_sc1(&a.desc[tile], ((uint64_t)a.tag << 32) | tc);
+    if (tid < 64) {  // look-back over tiles 0 .. tile-1, 64 per round trip
+        uint64_t P = 0;
+        for (uint32_t i0 = 0; i0 < tile; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            uint64_t d = i < tile ? ld_sc1(&a.desc[i]) : 0ull;
+            bool pend = i < tile && (uint32_t)(d >> 32) != a.tag;
+            for (uint32_t spins = 0; __ballot(pend); ++spins) {
+                __builtin_amdgcn_s_sleep(4);
+                if (pend) {
+                    d = ld_sc1(&a.desc[i]);
+                    pend = (uint32_t)(d >> 32) != a.tag;
+                }
+                if (spins > (1u << 20)) { if (lane == 0) s_bad = 1; break; }  // ~0.3 s: give up, poison the count
+            }
+            P += (uint32_t)d;
+        }
+        P = wave_sum64(P);
+        if (lane == 0) s_P = P;
+    }
+    __syncthreads();
+    const uint64_t P = s_P;
+#pragma unroll
+    for (uint32_t b = 0; b < WPER; ++b) {
+        if (keep >> b & 1u) {
+            a.out_idx[P + r] = j[b];
+            a.out_val[P + r] = (0.0f + v[b]) / 1.0f;
+            a.win[j[b]] = 0;  // scratch back to zero for the next call
+            ++r;
+        }
+    }
+    if (tid == 0 && tile == a.ntiles - 1) *a.out_count = s_bad ? 0xffffffffu : (uint32_t)(P + tc);
+}
+
 __global__ void __launch_bounds__(STG_WG) sgd_apply(SgdLaunch a) {
     uint32_t len = a.grad_len;
     if (a.d_grad_len) len = min(len, *a.d_grad_len);
@@ -480,13 +559,19 @@ hipError_t launch_error_feedback(float *grad, size_t n, const uint32_t *idx, siz
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,
                                 uint32_t *out_count, uint32_t *scratch_tiles, uint32_t *win, int num_cu,
-                                hipStream_t s) {
+                                hipStream_t s, const Win1Desc &w1) {
     const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((per_rank + STG_WG - 1) / STG_WG,
                                                                           (size_t)num_cu * 8));
     if (world == 1) {
         if (!per_rank) return hipMemsetAsync(out_count, 0, sizeof(uint32_t), s);
         win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win);
         const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
+        if (w1.desc) {  // count and emit in one launch (tagged tile counts, look-back)
+            Win1Args a{idx, val, per_rank, n, nt, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count};
+            win_emit1t<<<nt, STG_WG, 0, s>>>(a);
+            if (w1.grid_out) *w1.grid_out = nt;
+            return hipGetLastError();
+        }
         win_count<<<nt, STG_WG, 0, s>>>(idx, per_rank, n, win, scratch_tiles);
         const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)num_cu, nt));
         win_emit1<<<G, STG_WG, 0, s>>>(idx, val, per_rank, n, nt, win, scratch_tiles, out_idx, out_val, out_count);

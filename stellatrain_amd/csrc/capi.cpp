@@ -527,6 +527,11 @@ struct MergeScratch {
     int device = 0;
     uint32_t *tiles = nullptr, *win = nullptr;
     size_t cap_tiles = 0, cap_win = 0;
+    // world == 1 in one launch: tagged per-tile counts (cap_tiles of them, zeroed
+    // whenever reallocated), the tile ticket and its value at the next call
+    uint64_t *desc = nullptr, *ticket = nullptr;
+    uint64_t tbase = 0;
+    uint32_t tag = 0;
 };
 std::mutex g_merge_mu;
 std::map<std::pair<int, hipStream_t>, std::unique_ptr<MergeScratch>> g_merge;
@@ -546,7 +551,16 @@ int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_ra
         (void)hipFree(m->tiles);
         m->tiles = nullptr;
         HIP_TRY(hipMalloc(&m->tiles, tiles * sizeof(uint32_t)));
+        (void)hipFree(m->desc);
+        m->desc = nullptr;
+        HIP_TRY(hipMalloc(&m->desc, tiles * sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(m->desc, 0, tiles * sizeof(uint64_t), s));  // no stale tags
         m->cap_tiles = tiles;
+    }
+    if (!m->ticket) {
+        HIP_TRY(hipMalloc(&m->ticket, sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(m->ticket, 0, sizeof(uint64_t), s));
+        m->tbase = 0;
     }
     const size_t words = std::max<size_t>(n, 1);
     if (words > m->cap_win) {
@@ -836,8 +850,12 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
     std::lock_guard<std::mutex> g(ms->mu);
     int rc = merge_scratch_ensure(ms, s, n, per_rank);
     if (rc) return rc;
+    if (++ms->tag == 0) ms->tag = 1;
+    uint32_t grid = 0;
+    const stg::Win1Desc w1{ms->desc, ms->ticket, ms->tbase, ms->tag, &grid};
     HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, n, d_dense, d_mark, d_out_idx, d_out_val,
-                                      d_out_count, ms->tiles, ms->win, ncu, s));
+                                      d_out_count, ms->tiles, ms->win, ncu, s, w1));
+    ms->tbase += grid;
     return STG_OK;
 }
 

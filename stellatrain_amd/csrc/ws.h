@@ -188,10 +188,20 @@ hipError_t launch_radix_level1(const float *a, size_t m, uint32_t last_mask, uin
 
 hipError_t launch_synth(float *dst, size_t n, uint64_t seed, int dist, uint32_t param, hipStream_t s);
 
+// world == 1 in one launch after the winner election: tagged per-tile counts
+// and a ticket counter of the (device, stream) scratch (desc == nullptr: the
+// two-launch count / emit instead)
+struct Win1Desc {
+    uint64_t *desc;       // per tile {tag:32 | winners:32}, zero at creation
+    uint64_t *ticket;     // monotonic tile counter, zero at creation
+    uint64_t base;        // its value when the call starts
+    uint32_t tag;         // call tag >= 1
+    uint32_t *grid_out;   // receives the tiles launched (the ticket advances by it)
+};
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,
                                 uint32_t *out_count, uint32_t *scratch_tiles, uint32_t *win, int num_cu,
-                                hipStream_t s);
+                                hipStream_t s, const Win1Desc &w1);
 constexpr uint32_t MERGE_TILE = STG_WG * 16;  // pairs / marks per scatter-merge tile
 
 struct SgdLaunch {
