@@ -209,10 +209,10 @@ __device__ __forceinline__ uint32_t rf_key(uint32_t pos) {
 // offset cnt + 16 i (less 16 - tl after the tail), at most rem elements.  Four
 // lanes per line (a float4 each: one 64-byte request per line), eight rounds
 // of loads in flight before their stores.
-template <typename GetPos>
+template <uint32_t K = 5, typename GetPos>
 __device__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np, uint32_t tail_rank,
                            GetPos pos_of) {
-    constexpr uint32_t K = 5, LPR = FILL_WG / 4;  // rounds in flight, lines per round
+    constexpr uint32_t LPR = FILL_WG / 4;  // lines per round; K rounds of loads in flight
     const bool vec = aligned16(d) && (cnt & 3u) == 0;
     const uint32_t q = threadIdx.x & 3u;
     auto span = [&](uint32_t i, uint32_t &off, uint32_t &len) {  // output offset and length of entry i
@@ -363,7 +363,11 @@ __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uin
 // SIMD run beside the six of two scan workgroups.  The LDS is dynamic: the
 // compiler derives the occupancy it aims for from static LDS and would widen
 // the register budget to the one workgroup per CU that 88 KiB alone allows.
-__global__ void __launch_bounds__(FILL_WG) __attribute__((amdgpu_waves_per_eu(8, 8)))
+// LONE: the launch's only bucket(s), nothing co-resident to share the CU
+// with: 4 waves per SIMD (128 VGPRs), the whole window prefetched (no second
+// round trip for its tail) and twice the emission loads in flight.
+template <bool LONE>
+__global__ void __launch_bounds__(FILL_WG) __attribute__((amdgpu_waves_per_eu(LONE ? 4 : 8, 8)))
 tv16_fill(Tv16FillArgs A) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fill_lds[];
     FillLds &S = *reinterpret_cast<FillLds *>(fill_lds);
@@ -385,7 +389,8 @@ tv16_fill(Tv16FillArgs A) {
     // the scan launch has finished: every word is final, read them together,
     // with the first PRE window entries (most buckets have fewer) ahead of
     // knowing how many there are
-    constexpr uint32_t PRE = 8, PREX = 8;  // keys / lines and indices prefetched per thread
+    constexpr uint32_t PRE = LONE ? 10 : 8, PREX = PRE;  // keys / lines and indices prefetched per thread
+    constexpr uint32_t KE = LONE ? 10 : 5;                 // emission rounds in flight (> 10: the compiler spills x[])
     const uint32_t *cu = d.cand, *cl = d.cand + CAND_CAP, *ci = d.cand + 2 * CAND_CAP;
     uint32_t pk[PRE], pl[PREX], pc[PREX];
 #pragma unroll
@@ -542,7 +547,7 @@ tv16_fill(Tv16FillArgs A) {
         fast = covered >= rem;
         if (!fast && tid == 0) atomicAdd(&A.dbg[63], 1u);
         if (fast && !ties) {  // distinct sums: the heap pops them in sum order
-            emit_order(d, cnt, rem, P0, tail_rank0, line_lds);
+            emit_order<KE>(d, cnt, rem, P0, tail_rank0, line_lds);
             count_path(0);
             stamp(5);
             return;
@@ -645,7 +650,7 @@ tv16_fill(Tv16FillArgs A) {
                 uint32_t P, tail_rank;
                 pops(P, tail_rank);
                 stamp(0);
-                emit_order(d, cnt, rem, P, tail_rank, line_lds);
+                emit_order<KE>(d, cnt, rem, P, tail_rank, line_lds);
                 count_path(1);
                 stamp(0);
                 stamp(2);
@@ -880,7 +885,7 @@ tv16_fill(Tv16FillArgs A) {
             if (STG_FILL_STAMPS && tid == 0 && b == 0) A.dbg[45] = P;
             // the pops never reinsert an element of R (see (2) above)
             if (S.maxpos + P < N && P <= Rn) {
-                emit_order(d, cnt, rem, P, tail_rank, line_of);
+                emit_order<KE>(d, cnt, rem, P, tail_rank, line_of);
                 count_path(2);
                 stamp(1);
                 return;
@@ -901,11 +906,16 @@ tv16_fill(Tv16FillArgs A) {
 
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {
     if (!a.nbk) return hipSuccess;
-    static const hipError_t attr =
-        hipFuncSetAttribute(reinterpret_cast<const void *>(&tv16_fill), hipFuncAttributeMaxDynamicSharedMemorySize,
+    static const hipError_t attr0 =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&tv16_fill<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(FillLds));
-    if (attr != hipSuccess) return attr;
-    tv16_fill<<<a.nbk, FILL_WG, sizeof(FillLds), s>>>(a);
+    static const hipError_t attr1 =
+        hipFuncSetAttribute(reinterpret_cast<const void *>(&tv16_fill<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(FillLds));
+    if (attr0 != hipSuccess) return attr0;
+    if (attr1 != hipSuccess) return attr1;
+    if (a.lone) tv16_fill<true><<<a.nbk, FILL_WG, sizeof(FillLds), s>>>(a);
+    else tv16_fill<false><<<a.nbk, FILL_WG, sizeof(FillLds), s>>>(a);
     return hipGetLastError();
 }
 

@@ -141,6 +141,7 @@ struct Tv16FillArgs {
     uint32_t *fail;
     uint32_t *dbg;         // diagnostics: phase stamps of workgroup 0 (ws.misc)
     uint32_t mode;         // tests (STG_DEBUG_TV16_FILL): 1 = always the shadow heap, 2 = always the literal heap
+    bool lone;             // a one-bucket launch: the fill variant that takes the CU's registers
 };
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
 
