@@ -802,7 +802,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         static const uint32_t fill_mode =
             getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
         F.mode = fill_mode;
-        F.lone = a.nb == 1;
+        static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
+        F.lone = lone_ok && a.nb == 1;
         const hipError_t e = launch_tv16_fill(F, s);
         if (e != hipSuccess) return e;
     }
