@@ -27,9 +27,16 @@ namespace {
 constexpr uint32_t NCOPY = STG_RS_NCOPY;
 constexpr uint32_t HWG = 1024;  // rs_hist workgroup: one fat workgroup per CU, few global bin atomics
 
+#ifndef STG_RS_STAMPS
+#define STG_RS_STAMPS 0  // diagnostics: level-1 phase times (100 MHz clock) into dbg[24..31]
+#endif
+
 template <int SHIFT, int NBITS>
 __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size_t m, uint32_t last_mask,
-                                               RSel *st, uint64_t extra_zeros, uint32_t rank) {
+                                               RSel *st, uint64_t extra_zeros, uint32_t rank, uint32_t *dbg) {
+    constexpr bool STAMPS = STG_RS_STAMPS && SHIFT == 20;
+    auto now = [] { return (uint32_t)__builtin_amdgcn_s_memrealtime(); };
+    if (STAMPS && threadIdx.x == 0) { const uint32_t t = now(); atomicMax(&dbg[24], ~t); atomicMax(&dbg[25], t); }
     constexpr bool FIRST = SHIFT + NBITS == 31;
     constexpr uint32_t NB = 1u << NBITS;
     // copies one word apart in the bank order (a stride of NB words would put
@@ -95,13 +102,29 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
         }
     }
     __syncthreads();
+    if (STAMPS && threadIdx.x == 0) atomicMax(&dbg[26], now());  // streaming done
     for (uint32_t i = threadIdx.x; i < NB; i += HWG) {
         uint32_t c = 0;
 #pragma unroll
         for (uint32_t q = 0; q < NCOPY; ++q) c += h[q][i];
         if (c) g_add(&st->hist[blockIdx.x % RS_SH_HIST][i], c);
     }
-    if (last_workgroup(st)) pick_level<SHIFT, NBITS, HWG, RS_SH_HIST>(st, extra_zeros, rank);
+    if (STAMPS) { __syncthreads(); if (threadIdx.x == 0) atomicMax(&dbg[27], now()); }  // flushed
+    if (last_workgroup(st)) {
+        const uint32_t t0 = now();
+        pick_level<SHIFT, NBITS, HWG, RS_SH_HIST>(st, extra_zeros, rank);
+        if (STAMPS) {
+            __syncthreads();
+            if (threadIdx.x == 0) {  // this call's record at [32..37], accumulators reset
+                dbg[32] = ~atomicExch(&dbg[24], 0u);
+                dbg[33] = atomicExch(&dbg[25], 0u);
+                dbg[34] = atomicExch(&dbg[26], 0u);
+                dbg[35] = atomicExch(&dbg[27], 0u);
+                dbg[36] = t0;
+                dbg[37] = now();
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -110,9 +133,9 @@ hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uin
                                const DevWS &ws, int num_cu, hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
     const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
-    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
-    rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
-    rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
+    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
+    rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
+    rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
     return hipGetLastError();
 }
 
@@ -122,7 +145,7 @@ hipError_t launch_radix_level1(const float *a, size_t m, uint32_t last_mask, uin
                                const DevWS &ws, int num_cu, hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
     const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
-    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank);
+    rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
     return hipGetLastError();
 }
 
