@@ -254,29 +254,6 @@ __device__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, 
     }
 }
 
-// The orderer's emission of the pops' order: with helper workgroups (a lone
-// bucket), publish the order's line positions and the pop count, then emit
-// share 0; the helpers emit the other shares.
-template <uint32_t KE, bool LONE, typename GetPos>
-__device__ __forceinline__ void emit_all(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t P,
-                                         uint32_t tail_rank, GetPos pos_of, uint32_t nhelp, CallCtl *ccp,
-                                         uint32_t *order_g, uint32_t ready_tag) {
-    if (LONE && nhelp) {
-        for (uint32_t i = threadIdx.x; i < P; i += FILL_WG) st_sc1(&order_g[i], pos_of(i));
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            st_sc1(&ccp->pad[2], P);
-            st_sc1(&ccp->pad[3], tail_rank);
-            __builtin_amdgcn_s_waitcnt(0);
-            st_sc1(&ccp->pad[1], ready_tag);
-        }
-        emit_order<KE>(d, cnt, rem, P, tail_rank, pos_of, 0, (P + nhelp) / (nhelp + 1));
-    } else {
-        emit_order<KE>(d, cnt, rem, P, tail_rank, pos_of);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // full path: the literal algorithm on the whole candidate vector
 // ---------------------------------------------------------------------------
@@ -421,54 +398,6 @@ tv16_fill(Tv16FillArgs A) {
     stamp(0);
     const Tv16FillBucket &d = A.bk[b];
     const Decision &D = A.dec[b];
-    uint32_t *const order_g = const_cast<uint32_t *>(d.cand) + 3 * CAND_CAP;  // the spare window array: the order
-    const uint32_t ready_tag = (A.epoch << 8) | 0x5au;
-    if (LONE && role) {  // a helper: wait for the orderer's pop order, emit share `role` of it
-        const uint64_t h0 = ld_sc1(&D.w[0]), h1 = ld_sc1(&D.w[1]);
-        if ((uint32_t)(h0 >> 32) != ((A.epoch << 8) | TV16_TAG_DEC) || !((uint32_t)h0 & TV16_DEC_B) ||
-            ld_sc1(A.fail) || role > A.helpers)
-            return;  // no regime-B fill (or the scan failed): nothing to emit
-        if (!(uint32_t)h1 && !((uint32_t)h0 & TV16_DEC_TAIL)) return;  // nothing missing (the orderer returns too)
-        uint64_t st0 = 0;
-        for (uint32_t spins = 0; ld_sc1(&A.cc->pad[1]) != ready_tag; ++spins) {
-            __builtin_amdgcn_s_sleep(4);
-            if (spin_expired(spins, st0)) {
-                if (tid == 0) { g_or(A.fail, FAIL_SPIN_TIMEOUT); st_sc1(d.count_out, POISON_COUNT); }
-                return;
-            }
-        }
-        const uint32_t P = ld_sc1(&A.cc->pad[2]), tail_rank = ld_sc1(&A.cc->pad[3]);
-        const uint32_t nsh = A.helpers + 1u, chunk = (P + nsh - 1) / nsh;
-        const uint32_t cnt = (uint32_t)(h1 >> 32), rem = d.dst_len - cnt;
-        // the share [i0, i1) of the order, as emit_order writes it (scalars
-        // taken out of the argument block first: emitting through a reference
-        // to it here made the compiler copy the whole block to scratch)
-        const float *src = d.src;
-        uint32_t *oidx = d.idx;
-        float *oval = d.val;
-        const uint32_t tl = d.tl, ioff = (uint32_t)d.idx_offset;
-        const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(oidx) |
-                           reinterpret_cast<uintptr_t>(oval)) & 15u) == 0 && (cnt & 3u) == 0;
-        const uint32_t i1 = min(P, (role + 1) * chunk), q = tid & 3u;
-        for (uint32_t i = role * chunk + (tid >> 2); i < i1; i += FILL_WG / 4) {
-            const uint32_t o16 = 16u * i - (tail_rank < i ? 16u - tl : 0u);
-            if (o16 >= rem) continue;
-            const uint32_t len = min(i == tail_rank ? tl : 16u, rem - o16);
-            const uint32_t pos = ld_sc1(&order_g[i]), o = cnt + o16 + 4 * q, bi = pos + 4 * q + ioff;
-            if (vec && len == 16 && (o16 & 3u) == 0) {
-                *reinterpret_cast<float4 *>(oval + o) = reinterpret_cast<const float4 *>(src + (size_t)pos)[q];
-                *reinterpret_cast<uint4 *>(oidx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
-            } else {
-                for (uint32_t c = 0; c < 4; ++c) {
-                    if (4 * q + c < len) {
-                        oval[o + c] = src[(size_t)pos + 4 * q + c];
-                        oidx[o + c] = bi + c;
-                    }
-                }
-            }
-        }
-        return;
-    }
     // the scan launch has finished: every word is final, read them together,
     // with the first PRE window entries (most buckets have fewer) ahead of
     // knowing how many there are
@@ -503,8 +432,42 @@ tv16_fill(Tv16FillArgs A) {
     const uint32_t N = d.nb - Qtot + (tail ? 1u : 0u);  // candidate vector length
     const uint32_t rem = d.dst_len - cnt;
     if (!M && !tail) return;
-    const uint32_t nhelp = LONE ? A.helpers : 0u;
-    CallCtl *const ccp = A.cc;
+    uint32_t *const order_g = const_cast<uint32_t *>(d.cand) + 3 * CAND_CAP;  // the spare window array: the order
+    const uint32_t ready_tag = (A.epoch << 8) | 0x5au;
+    const uint32_t nshare = 1u + (LONE ? A.helpers : 0u);
+    if (LONE && role) {  // a helper: wait for the order, emit share `role`
+        if (role >= nshare) return;
+        uint64_t st0 = 0;
+        for (uint32_t spins = 0; ld_sc1(&A.cc->pad[1]) != ready_tag; ++spins) {
+            __builtin_amdgcn_s_sleep(4);
+            if (spin_expired(spins, st0)) {
+                if (tid == 0) { g_or(A.fail, FAIL_SPIN_TIMEOUT); st_sc1(d.count_out, POISON_COUNT); }
+                return;
+            }
+        }
+        const uint32_t P = ld_sc1(&A.cc->pad[2]), tail_rank = ld_sc1(&A.cc->pad[3]);
+        const uint32_t chunk = (P + nshare - 1) / nshare;
+        emit_order<KE>(d, cnt, rem, P, tail_rank, [order_g](uint32_t i) { return ld_sc1(&order_g[i]); }, role * chunk,
+                       (role + 1) * chunk);
+        return;
+    }
+    // The orderer's emission: with helpers, publish the order and emit share 0.
+    auto emit_all = [&](uint32_t P, uint32_t tail_rank, auto pos_of) __attribute__((always_inline)) {
+        if (LONE && A.helpers) {
+            for (uint32_t i = tid; i < P; i += FILL_WG) st_sc1(&order_g[i], pos_of(i));
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+            if (tid == 0) {
+                st_sc1(&A.cc->pad[2], P);
+                st_sc1(&A.cc->pad[3], tail_rank);
+                __builtin_amdgcn_s_waitcnt(0);
+                st_sc1(&A.cc->pad[1], ready_tag);
+            }
+            emit_order<KE>(d, cnt, rem, P, tail_rank, pos_of, 0, (P + nshare - 1) / nshare);
+        } else {
+            emit_order<KE>(d, cnt, rem, P, tail_rank, pos_of);
+        }
+    };
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
     const bool tail_in = tail && tail_key >= u2f(wlo);
@@ -632,7 +595,7 @@ tv16_fill(Tv16FillArgs A) {
         fast = covered >= rem;
         if (!fast && tid == 0) atomicAdd(&A.dbg[63], 1u);
         if (fast && !ties) {  // distinct sums: the heap pops them in sum order
-            emit_all<KE, LONE>(d, cnt, rem, P0, tail_rank0, line_lds, nhelp, ccp, order_g, ready_tag);
+            emit_all(P0, tail_rank0, line_lds);
             count_path(0);
             stamp(5);
             return;
@@ -735,7 +698,7 @@ tv16_fill(Tv16FillArgs A) {
                 uint32_t P, tail_rank;
                 pops(P, tail_rank);
                 stamp(0);
-                emit_all<KE, LONE>(d, cnt, rem, P, tail_rank, line_lds, nhelp, ccp, order_g, ready_tag);
+                emit_all(P, tail_rank, line_lds);
                 count_path(1);
                 stamp(0);
                 stamp(2);
@@ -970,7 +933,7 @@ tv16_fill(Tv16FillArgs A) {
             if (STG_FILL_STAMPS && tid == 0 && b == 0) A.dbg[45] = P;
             // the pops never reinsert an element of R (see (2) above)
             if (S.maxpos + P < N && P <= Rn) {
-                emit_all<KE, LONE>(d, cnt, rem, P, tail_rank, line_of, nhelp, ccp, order_g, ready_tag);
+                emit_all(P, tail_rank, line_of);
                 count_path(2);
                 stamp(1);
                 return;

@@ -804,6 +804,10 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.mode = fill_mode;
         static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
         F.lone = lone_ok && a.nb == 1;
+        static const uint32_t helpers =
+            getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
+        F.helpers = F.lone ? std::min(helpers, 63u) : 0u;
+        F.cc = &ws.ctl->cc[a.epoch & 1u];
         const hipError_t e = launch_tv16_fill(F, s);
         if (e != hipSuccess) return e;
     }

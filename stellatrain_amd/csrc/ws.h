@@ -142,6 +142,8 @@ struct Tv16FillArgs {
     uint32_t *dbg;         // diagnostics: phase stamps of workgroup 0 (ws.misc)
     uint32_t mode;         // tests (STG_DEBUG_TV16_FILL): 1 = always the shadow heap, 2 = always the literal heap
     bool lone;             // a one-bucket launch: the fill variant that takes the CU's registers
+    uint32_t helpers;      // lone: extra workgroups that emit shares of the order (0: none)
+    CallCtl *cc;           // this call's counters: [pad 0] fill tickets, [1] order ready, [2] pops, [3] tail rank
 };
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
 
