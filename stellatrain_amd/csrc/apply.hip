@@ -71,16 +71,29 @@ __global__ void __launch_bounds__(STG_WG) win_emit1(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ out_idx, float *__restrict__ out_val,
                                                     uint32_t *out_count);
 
-__global__ void __launch_bounds__(STG_WG) scatter_rank(const uint32_t *__restrict__ idx, const float *__restrict__ val,
-                                                       size_t m, size_t n, uint32_t *__restrict__ win,
+// world > 1: rank r's scatter and rank r+1's winner election in one launch,
+// on the two halves of the election scratch (rank parity), so a rank's
+// election never sees the previous rank's words: threads [0, m) scatter rank
+// `sr` (if any), threads [m, 2m) elect rank `mr` (if any).
+__global__ void __launch_bounds__(STG_WG) scatter_mark(const uint32_t *__restrict__ sidx, const float *__restrict__ sval,
+                                                       uint32_t *__restrict__ swin, const uint32_t *__restrict__ midx,
+                                                       uint32_t *__restrict__ mwin, size_t m, size_t n,
                                                        float *__restrict__ dense, uint8_t *__restrict__ mark) {
     const size_t stride = (size_t)gridDim.x * STG_WG;
-    for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
-        const uint32_t j = idx[i];
-        if (j >= n || win[j] != (uint32_t)i + 1u) continue;  // a later occurrence wins
-        win[j] = 0;
-        dense[j] += val[i];
-        mark[j] = 1;
+    for (size_t t = (size_t)blockIdx.x * STG_WG + threadIdx.x; t < 2 * m; t += stride) {
+        if (t < m) {
+            if (!sidx) continue;
+            const uint32_t j = sidx[t];
+            if (j >= n || swin[j] != (uint32_t)t + 1u) continue;  // a later occurrence wins
+            swin[j] = 0;
+            dense[j] += sval[t];
+            mark[j] = 1;
+        } else {
+            if (!midx) continue;
+            const size_t i = t - m;
+            const uint32_t j = midx[i];
+            if (j < n) atomicMax(&mwin[j], (uint32_t)i + 1u);
+        }
     }
 }
 
@@ -117,44 +130,73 @@ __global__ void __launch_bounds__(STG_WG) mark_count(const uint8_t *__restrict__
     }
 }
 
-__global__ void __launch_bounds__(STG_WG) mark_emit(uint8_t *__restrict__ mark, float *__restrict__ dense, size_t n,
-                                                    uint32_t ntiles, float world, const uint32_t *__restrict__ tile_cnt,
-                                                    uint32_t *__restrict__ out_idx, float *__restrict__ out_val,
-                                                    uint32_t *out_count) {
-    __shared__ uint64_t sh64[STG_WAVES];
-    __shared__ uint32_t sh[STG_WAVES + 1];
-    const uint32_t G = gridDim.x, w = blockIdx.x, tid = threadIdx.x;
-    const uint32_t t_begin = (uint32_t)((uint64_t)w * ntiles / G);
-    const uint32_t t_end = (uint32_t)((uint64_t)(w + 1) * ntiles / G);
-    uint64_t tot = 0, bef = 0;
-    for (uint32_t i = tid; i < ntiles; i += STG_WG) {
-        const uint32_t c = tile_cnt[i];
-        tot += c;
-        if (i < t_begin) bef += c;
+// Exclusive prefixes of the per-tile mark counts at [ntiles + t] and the total
+// in *out_count (one 1024-thread workgroup, 4 tiles per thread per round).
+__global__ void __launch_bounds__(1024) mark_scan(uint32_t *__restrict__ tile_cnt, uint32_t ntiles,
+                                                  uint32_t *out_count) {
+    __shared__ uint32_t sh[16 + 1];
+    uint32_t run = 0;
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += 4 * 1024) {
+        const uint32_t tb = t0 + 4 * threadIdx.x;
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) { c[q] = tb + q < ntiles ? tile_cnt[tb + q] : 0u; sum += c[q]; }
+        uint32_t tot;
+        uint32_t p = run + blk_excl_scan<16>(sum, sh, &tot);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            if (tb + q < ntiles) { tile_cnt[ntiles + tb + q] = p; p += c[q]; }
+        run += tot;
     }
-    const uint64_t total = wg_sum64(tot, sh64);
-    uint64_t P = wg_sum64(bef, sh64);
-    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-        const size_t e = (size_t)tile * MARK_TILE + 16 * tid;
-        const uint4 v = load_marks(mark, n, e);
-        const uint32_t words[4] = {v.x, v.y, v.z, v.w};
-        uint32_t c = nz_bytes(v.x) + nz_bytes(v.y) + nz_bytes(v.z) + nz_bytes(v.w);
-        uint32_t tc;
-        uint32_t r = wg_excl_scan(c, sh, &tc);
-        for (uint32_t b = 0; b < 16; ++b) {
-            if ((words[b >> 2] >> (8 * (b & 3))) & 0xffu) {
-                const size_t j = e + b;
-                out_idx[P + r] = (uint32_t)j;
-                out_val[P + r] = dense[j] / world;
-                dense[j] = 0.f;  // leave the scratch zeroed for the next call
-                mark[j] = 0;
-                ++r;
-            }
-        }
-        P += tc;
-    }
-    if (w == 0 && tid == 0) *out_count = (uint32_t)total;
+    if (threadIdx.x == 0) *out_count = run;
 }
+
+// One workgroup per tile of MARK_TILE marks: the marked indices in order at
+// the tile's prefix, value dense / world; dense and marks zeroed behind it.
+// A lane's 16 marks and 16 dense values are one uint4 and four float4 loads.
+__global__ void __launch_bounds__(STG_WG) mark_emit_tile(uint8_t *__restrict__ mark, float *__restrict__ dense,
+                                                         size_t n, uint32_t ntiles, float world,
+                                                         const uint32_t *__restrict__ tile_cnt,
+                                                         uint32_t *__restrict__ out_idx, float *__restrict__ out_val) {
+    __shared__ uint32_t sh[STG_WAVES + 1];
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    if (!tile_cnt[tile]) return;  // uniform: nothing marked in this tile
+    const uint64_t P = tile_cnt[ntiles + tile];
+    const size_t e = (size_t)tile * MARK_TILE + 16 * tid;
+    const uint4 v = load_marks(mark, n, e);
+    const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t c = nz_bytes(v.x) + nz_bytes(v.y) + nz_bytes(v.z) + nz_bytes(v.w);
+    const bool full = e + 16 <= n;
+    float d[16];
+    if (c && full) {
+        const float4 *p = reinterpret_cast<const float4 *>(dense + e);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const float4 x = p[q];
+            d[4 * q] = x.x; d[4 * q + 1] = x.y; d[4 * q + 2] = x.z; d[4 * q + 3] = x.w;
+        }
+    }
+    uint32_t tc;
+    uint32_t r = wg_excl_scan(c, sh, &tc);
+    if (!c) return;
+#pragma unroll
+    for (uint32_t b = 0; b < 16; ++b) {
+        if ((words[b >> 2] >> (8 * (b & 3))) & 0xffu) {
+            const size_t j = e + b;
+            out_idx[P + r] = (uint32_t)j;
+            out_val[P + r] = (full ? d[b] : dense[j]) / world;
+            if (!full) { dense[j] = 0.f; mark[j] = 0; }
+            ++r;
+        }
+    }
+    if (full) {  // leave the scratch zeroed for the next call
+        float4 *p = reinterpret_cast<float4 *>(dense + e);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) p[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<uint4 *>(mark + e) = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
 
 constexpr uint32_t WPER = MARK_TILE / STG_WG;  // 16 consecutive pairs per lane
 static_assert(WPER == 16, "four uint4 of indices per lane");
@@ -577,16 +619,26 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
         win_emit1<<<G, STG_WG, 0, s>>>(idx, val, per_rank, n, nt, win, scratch_tiles, out_idx, out_val, out_count);
         return hipGetLastError();
     }
-    for (int r = 0; r < world; ++r) {
-        if (!per_rank) break;
-        const uint32_t *ir = idx + (size_t)r * per_rank;
-        win_mark<<<blocks, STG_WG, 0, s>>>(ir, per_rank, n, win);
-        scatter_rank<<<blocks, STG_WG, 0, s>>>(ir, val + (size_t)r * per_rank, per_rank, n, win, dense, mark);
+    // rank r's scatter beside rank r+1's election (parity halves of `win`,
+    // which holds 2n words for world > 1): world + 1 launches instead of 2 world
+    if (per_rank) {
+        const uint32_t b2 = (uint32_t)std::max<size_t>(1, std::min<size_t>((2 * per_rank + STG_WG - 1) / STG_WG,
+                                                                           (size_t)num_cu * 8));
+        for (int r = 0; r <= world; ++r) {
+            const bool sc = r >= 1, mk = r < world;
+            const size_t ps = (size_t)(r - 1) * per_rank, pm = (size_t)r * per_rank;
+            scatter_mark<<<b2, STG_WG, 0, s>>>(sc ? idx + ps : nullptr, sc ? val + ps : nullptr,
+                                               win + (size_t)((r - 1) & 1) * n, mk ? idx + pm : nullptr,
+                                               win + (size_t)(r & 1) * n, per_rank, n, dense, mark);
+        }
     }
     const uint32_t ntiles = (uint32_t)((n + MARK_TILE - 1) / MARK_TILE);
-    mark_count<<<std::max<uint32_t>(1, ntiles), STG_WG, 0, s>>>(mark, n, scratch_tiles);
-    const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)num_cu, ntiles));
-    mark_emit<<<G, STG_WG, 0, s>>>(mark, dense, n, ntiles, (float)world, scratch_tiles, out_idx, out_val, out_count);
+    if (!ntiles) return hipMemsetAsync(out_count, 0, sizeof(uint32_t), s);
+    // per-tile counts, their scan, then one workgroup per tile (the old
+    // mark_emit walked its tiles one after another: ~90 us at 64 MiB)
+    mark_count<<<ntiles, STG_WG, 0, s>>>(mark, n, scratch_tiles);
+    mark_scan<<<1, 1024, 0, s>>>(scratch_tiles, ntiles, out_count);
+    mark_emit_tile<<<ntiles, STG_WG, 0, s>>>(mark, dense, n, ntiles, (float)world, scratch_tiles, out_idx, out_val);
     return hipGetLastError();
 }
 

@@ -544,8 +544,9 @@ MergeScratch *merge_scratch(int dev, hipStream_t s) {
 }
 
 // Caller holds m->mu.
-int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_rank) {
-    const size_t tiles = (std::max(n, per_rank) + stg::MERGE_TILE - 1) / stg::MERGE_TILE + 1;
+int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_rank, int world) {
+    // per-tile counts and their prefixes (the world > 1 mark scan)
+    const size_t tiles = 2 * ((std::max(n, per_rank) + stg::MERGE_TILE - 1) / stg::MERGE_TILE) + 2;
     if (tiles > m->cap_tiles) {
         HIP_TRY(hipStreamSynchronize(s));
         (void)hipFree(m->tiles);
@@ -562,7 +563,7 @@ int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_ra
         HIP_TRY(hipMemsetAsync(m->ticket, 0, sizeof(uint64_t), s));
         m->tbase = 0;
     }
-    const size_t words = std::max<size_t>(n, 1);
+    const size_t words = std::max<size_t>(world > 1 ? 2 * n : n, 1);  // world > 1: two election halves
     if (words > m->cap_win) {
         HIP_TRY(hipStreamSynchronize(s));
         (void)hipFree(m->win);
@@ -848,7 +849,7 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
     hipStream_t s = static_cast<hipStream_t>(stream);
     MergeScratch *ms = merge_scratch(dev, s);
     std::lock_guard<std::mutex> g(ms->mu);
-    int rc = merge_scratch_ensure(ms, s, n, per_rank);
+    int rc = merge_scratch_ensure(ms, s, n, per_rank, world);
     if (rc) return rc;
     if (++ms->tag == 0) ms->tag = 1;
     uint32_t grid = 0;

@@ -289,6 +289,29 @@ def c5_round_trip(torch, steps, kind="sgd"):
             "GBps_dense_in": round(4.0 * n / us / 1e3, 1), "alg_GBps": round(alg / us / 1e3, 1)}
 
 
+def merge_world(torch, calls, world=8):
+    """MERGE decompress of `world` rank streams (cpu_optimize.cpp:40-72) into a
+    64 MiB bucket: k = 167,772 pairs per rank, each rank's indices a distinct
+    seeded sample of the bucket (overlapping across ranks)."""
+    from stellatrain_amd import merge_numel, scatter_merge
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = 16 << 20
+    k = merge_numel(n, 0.99)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    idx = torch.cat([torch.sort(torch.randperm(n, generator=g)[:k]).values for _ in range(world)]).to(torch.int32)
+    idx, val = idx.to(dev), torch.randn(world * k, generator=g).to(dev)
+    dense = torch.zeros(n, dtype=torch.float32, device=dev)
+    mark = torch.zeros(n, dtype=torch.uint8, device=dev)
+    oi = torch.empty(world * k, dtype=torch.int32, device=dev)
+    ov = torch.empty(world * k, dtype=torch.float32, device=dev)
+    oc = torch.empty(1, dtype=torch.int32, device=dev)
+    us = _time_loop(torch, st, lambda s: scatter_merge(idx, val, k, world, n, dense, mark, oi, ov, oc), calls, 8)
+    alg = world * 8.0 * k + 8.0 * int(oc.item()) + 5.0 * n  # pairs in, union out, dense + marks read once
+    return {"config": f"MERGE decompress world={world}, 64 MiB bucket, k={k} per rank", "us_per_call": round(us, 2),
+            "union": int(oc.item()), "alg_GBps": round(alg / us / 1e3, 1)}
+
+
 def _time_loop(torch, st, fn, calls, warmup):
     for s in range(warmup):
         fn(s)
@@ -435,7 +458,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
     p.add_argument("--c4-streams", type=int, default=4)
-    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,ef,gather")
+    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,merge,ef,gather")
     a = p.parse_args()
     os.environ.setdefault("STG_TV16_INFLIGHT", str(min(4, a.c4_streams)))
     import torch
@@ -463,6 +486,9 @@ def main():
     if "ef" in only:
         for d in merge_ef(torch, max(8, a.calls // 4)):
             emit(d)
+    if "merge" in only:
+        for w in (2, 8):
+            emit(merge_world(torch, a.calls, w))
     if "apply" in only:
         for d in apply_and_wire(torch, a.calls):
             emit(d)
