@@ -192,8 +192,10 @@ def _quantized(n, seed, step):
 # Ties at T: (a) ~1.3k equal keys in T's level-2 bin (the listed select);
 # (b) ~26k equal keys (more than the list holds: the level-3 histogram and the
 # one-workgroup recount); (c) 90 % zeros with k past the nonzeros (T = 0, every
-# tile past its superset capacity).
-@pytest.mark.parametrize("case", ["ties_listed", "ties_crowded", "zeros_t0"])
+# tile past its superset capacity); (d) magnitudes in ascending order: every
+# key of the top k sits in the last tiles (each of them overflows its
+# superset and is re-read).
+@pytest.mark.parametrize("case", ["ties_listed", "ties_crowded", "zeros_t0", "sorted"])
 @pytest.mark.parametrize("bug_compat", [False, True])
 def test_topk_ties(gpu, oracle, case, bug_compat):
     import torch
@@ -203,8 +205,11 @@ def test_topk_ties(gpu, oracle, case, bug_compat):
         src, k = _quantized(n, seed_for(13, 0), 5e-6), 10485
     elif case == "ties_crowded":
         src, k = _quantized(n, seed_for(13, 1), 1e-4), 10485
-    else:
+    elif case == "zeros_t0":
         src, k = synth(n, seed_for(13, 2), D3, 9000), 200000
+    else:
+        x = synth(n, seed_for(13, 3))
+        src, k = x[np.argsort(np.abs(x), kind="stable")], 10485
     if bug_compat:
         k = min(k, n // 8) if case != "zeros_t0" else n // 4 + 5000  # past the copied floats: T = 0
     co, io, vo = oracle.topk_compress(src, k, bug_compat=bug_compat)
