@@ -101,7 +101,14 @@ constexpr uint32_t GB = 512;        // chunk descriptors gathered per round trip
 // float4 loads in flight per streaming wave: 2 x 14 x 64 x 16 B x SCAN_D per CU
 // (SCAN_D = 3: 84 KiB per CU, just over the ~72 KiB that hides an HBM miss;
 // deeper queues add latency to every exchange round trip -- Little's law)
-constexpr uint32_t SCAN_D = STG_TV16_SCAN_D;
+constexpr uint32_t SCAN_D_BATCH = STG_TV16_SCAN_D;
+// A one-bucket launch (its fill runs after it, nothing else of the codec
+// beside it): each workgroup streams one chunk, so twice the loads in flight
+// halve its round trips; 6 waves per SIMD leave it ~80 VGPRs.
+#ifndef STG_TV16_SCAN_D_LONE
+#define STG_TV16_SCAN_D_LONE 6
+#endif
+constexpr uint32_t SCAN_D_LONE = STG_TV16_SCAN_D_LONE;
 constexpr uint32_t MAXG = 512;      // workgroups per launch (2 per CU)
 // ---------------------------------------------------------------------------
 // first call: sequential |x| sums per line, last partial line scaled by
@@ -240,7 +247,7 @@ constexpr uint32_t WIN = TV16_WIN;
 // scan of slot j = chunk k by streaming wave s: lines i = (s + NS*m)*16 +
 // lane/4 of the chunk, m = 0, 1, ...; SCAN_D float4 loads per lane in flight
 // through a buffer descriptor bounded to the chunk (lanes past it read zeros).
-template <int STAGE, bool EF>
+template <int STAGE, bool EF, uint32_t SCAN_D>
 __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint32_t s) {
     Lds &L = C.L;
     const uint32_t par = j % NBUF;
@@ -649,13 +656,14 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k) {
 // STAGE (diagnostics only, STG_DEBUG_TV16_STAGE): 0 = full codec; 1 = the
 // streaming waves' work only (the finisher releases buffers at once);
 // 3 = plain streaming read (calibration).
-template <int STAGE, bool EF>
+template <int STAGE, bool EF, bool LONE>
 // Registers for 8 waves per SIMD (<= 64 VGPRs): two workgroups per CU take 6
-// waves per SIMD and a fill workgroup's 2 run beside them.  The bound says
+// waves per SIMD and a fill workgroup's 2 run beside them (LONE: 6 waves per
+// SIMD, the fill comes after).  The bound says
 // 1024 threads (launches use FWG <= 1024) so that the compiler, which derives
 // the occupancy it aims for from the bound, does not widen the register
 // budget to the 6 waves two FWG-thread workgroups would give.
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LONE ? 6 : 8, 8)))
 tv16_batch(BatchArgs A) {
     __shared__ Lds L;
     Ctx C{A, L, gridDim.x, blockIdx.x, A.ctl, A.cand, A.fail};
@@ -700,7 +708,7 @@ tv16_batch(BatchArgs A) {
             const uint32_t k = uni(lds_ld(&L.cid[j % CIDR]));
             if (k >= A.K) break;
             asm volatile("" : "+s"(C.w), "+s"(C.G));
-            scan_chunk<STAGE, EF>(C, j, k, wave);
+            scan_chunk<STAGE, EF, LONE ? SCAN_D_LONE : SCAN_D_BATCH>(C, j, k, wave);
         }
     } else if (wave == FIN) {
         if (STG_TV16_PRIO) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
@@ -778,13 +786,16 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     // no more than there are chunks.  Co-residency is not required.
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(a.max_wg, K), MAXG));
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
+    static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
+    const bool lone_scan = lone_ok && a.nb == 1;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     switch (dbg_stage) {
-        case 1: tv16_batch<1, false><<<G, FWG, 0, s>>>(A); break;
-        case 3: tv16_batch<3, false><<<G, FWG, 0, s>>>(A); break;
+        case 1: tv16_batch<1, false, false><<<G, FWG, 0, s>>>(A); break;
+        case 3: tv16_batch<3, false, false><<<G, FWG, 0, s>>>(A); break;
         default:
-            if (ef) tv16_batch<0, true><<<G, FWG, 0, s>>>(A);
-            else tv16_batch<0, false><<<G, FWG, 0, s>>>(A);
+            if (ef) tv16_batch<0, true, false><<<G, FWG, 0, s>>>(A);
+            else if (lone_scan) tv16_batch<0, false, true><<<G, FWG, 0, s>>>(A);
+            else tv16_batch<0, false, false><<<G, FWG, 0, s>>>(A);
             break;
     }
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
@@ -802,8 +813,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         static const uint32_t fill_mode =
             getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
         F.mode = fill_mode;
-        static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
-        F.lone = lone_ok && a.nb == 1;
+        F.lone = lone_scan;
         static const uint32_t helpers =
             getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
         F.helpers = F.lone ? std::min(helpers, 63u) : 0u;
