@@ -23,14 +23,24 @@ namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
+// MAXS >= nsrc: every source's float4 is loaded before any is added (a
+// runtime-length loop of load-then-add waited for each load in turn), then
+// the sum runs in the reference's order: dst, residual, grad[1], ...
+template <uint32_t MAXS>
 __global__ void __launch_bounds__(STG_WG) gather_add_vec(GatherArgs a, size_t v0, size_t nv) {
     const size_t stride = (size_t)gridDim.x * STG_WG;
     for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < nv; i += stride) {
         const size_t e = v0 + 4 * i;
+        f4v x[MAXS];
         f4v acc = *reinterpret_cast<const f4v *>(a.dst + e);
-        if (a.resid) acc += __builtin_nontemporal_load(reinterpret_cast<const f4v *>(a.resid + e));
-        for (uint32_t s = 1; s < a.nsrc; ++s)
-            acc += __builtin_nontemporal_load(reinterpret_cast<const f4v *>(a.src[s] + e));
+        const f4v r = a.resid ? __builtin_nontemporal_load(reinterpret_cast<const f4v *>(a.resid + e)) : f4v{0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t s = 1; s < MAXS; ++s)
+            if (s < a.nsrc) x[s] = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(a.src[s] + e));
+        if (a.resid) acc += r;
+#pragma unroll
+        for (uint32_t s = 1; s < MAXS; ++s)
+            if (s < a.nsrc) acc += x[s];
         *reinterpret_cast<f4v *>(a.dst + e) = acc;
     }
 }
@@ -60,7 +70,9 @@ hipError_t launch_gather_add(const GatherArgs &a, size_t start, size_t end, int 
     const uint32_t cap = (uint32_t)num_cu * 8;
     if (nv) {
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((nv + STG_WG - 1) / STG_WG, cap));
-        gather_add_vec<<<blocks, STG_WG, 0, s>>>(a, v0, nv);
+        if (a.nsrc <= 4) gather_add_vec<4><<<blocks, STG_WG, 0, s>>>(a, v0, nv);
+        else if (a.nsrc <= 8) gather_add_vec<8><<<blocks, STG_WG, 0, s>>>(a, v0, nv);
+        else gather_add_vec<GATHER_MAX><<<blocks, STG_WG, 0, s>>>(a, v0, nv);
     }
     if (head) {
         const uint32_t blocks = (uint32_t)std::max<size_t>(1, std::min<size_t>((head + STG_WG - 1) / STG_WG, cap));
