@@ -13,6 +13,16 @@ def build_codec(jobs: int = 8) -> str:
     return os.path.join(HERE, "libstg_codec.so")
 
 
+def build_concurrency() -> str:
+    """tests/cpp/concurrency: T threads on one codec handle through the shim
+    (test binary, run by tests/test_gpu_concurrency.py on the GPU box)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "concurrency")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "concurrency.cpp"), "-o", exe, "-L", HERE, "-lstg_codec",
+                    "-lpthread", "-Wl,-rpath,$ORIGIN/../../stellatrain_amd"], check=True)
+    return exe
+
+
 def build_shim() -> str:
     """tests/cpp/shim_factory: the reference engine's codec factory and MERGE
     call site compiled against include/stg/compressor.h (test binary, run by
@@ -35,3 +45,4 @@ if __name__ == "__main__":
     print(build_codec())
     build_oracle()
     print(build_shim())
+    print(build_concurrency())

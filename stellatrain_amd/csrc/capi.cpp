@@ -24,7 +24,7 @@
 #include <unordered_map>
 #include <vector>
 
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include <dlfcn.h>
 
 #include "../../include/stg/codec.h"
 #include "ws.h"
@@ -615,16 +615,35 @@ namespace {
 // `rocprofv3 --marker-trace --kernel-trace` shows the host side of each call
 // next to its kernels.
 struct CritPath {
-    bool on;
-    CritPath() : on(enabled()) {
-        if (on) roctxRangePushA("CRIT_PATH_compress");
+    // the roctx library is opened only when STG_ROCTX=1 (no link-time
+    // dependency on rocprofiler-sdk for an opt-in diagnostic); a missing
+    // library leaves the ranges off
+    typedef int (*push_fn)(const char *);
+    typedef int (*pop_fn)();
+    struct Api {
+        push_fn push = nullptr;
+        pop_fn pop = nullptr;
+    };
+    const Api &api;
+    CritPath() : api(get()) {
+        if (api.push) api.push("CRIT_PATH_compress");
     }
     ~CritPath() {
-        if (on) roctxRangePop();
+        if (api.pop) api.pop();
     }
-    static bool enabled() {
-        static const bool v = getenv("STG_ROCTX") && atoi(getenv("STG_ROCTX")) == 1;
-        return v;
+    static const Api &get() {
+        static const Api a = [] {
+            Api r;
+            if (!(getenv("STG_ROCTX") && atoi(getenv("STG_ROCTX")) == 1)) return r;
+            void *h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) return r;
+            r.push = reinterpret_cast<push_fn>(dlsym(h, "roctxRangePushA"));
+            r.pop = reinterpret_cast<pop_fn>(dlsym(h, "roctxRangePop"));
+            if (!r.push || !r.pop) r = Api{};
+            return r;
+        }();
+        return a;
     }
 };
 }  // namespace

@@ -20,6 +20,7 @@ enum : uint32_t {
     FAIL_SPIN_TIMEOUT = 1u,   // a bounded grid-barrier / arrival spin gave up
     FAIL_CAND_OVERFLOW = 2u,  // regime-B candidate set exceeded the LDS sort capacity
     FAIL_LEVELS = 4u,         // regime-B radix descent did not converge
+    FAIL_SELECT = 8u,         // top-k: a winner ranked past k (select and tiles disagree)
 };
 
 namespace stg {

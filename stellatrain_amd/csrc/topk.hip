@@ -430,12 +430,23 @@ struct TkArgs {
     uint32_t *idx;
     float *val;
     uint32_t *count_out;
+    uint32_t *fail;      // the workspace's sticky failure word
     const RSel *rs;
     const uint32_t *tile_gt;
     const uint32_t *tile_eq;
     const uint2 *sup;
     const uint32_t *sup_n;
 };
+
+// A winner ranked past k: the select's counts and the tiles disagree (never
+// with a consistent select).  The write is dropped (kept in bounds), the
+// sticky failure word gets FAIL_SELECT and the count is poisoned, so the call
+// fails loudly (stg_codec_check, compress_host) instead of returning a short
+// stream with STG_OK.
+__device__ __forceinline__ void select_broken(const TkArgs &a) {
+    g_or(a.fail, FAIL_SELECT);
+    st_sc1(a.count_out, POISON_COUNT);
+}
 
 // One workgroup per tile: the winners (> T, then == T in index order until
 // k) at their prefix offsets, from the tile's superset.
@@ -474,7 +485,7 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
             for (uint32_t r = 0; r < 4; ++r) {
                 if ((qw >> r) & 1u) {
                     const uint64_t slot = win_before + wr++;
-                    if (slot >= a.k) continue;  // never with a consistent select; keeps a bad one in bounds
+                    if (slot >= a.k) { select_broken(a); continue; }  // an inconsistent select: surfaced
                     a.idx[slot] = a.bug_compat ? (uint32_t)slot : x[r].x + (uint32_t)a.idx_offset;
                     a.val[slot] = u2f(x[r].y);
                 }
@@ -513,7 +524,7 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
                     const uint32_t b = u * 4 + j;
                     if ((qw >> b) & 1u) {
                         const uint64_t slot = win_before + sw[b];
-                        if (slot >= a.k) continue;  // never with a consistent select; keeps a bad one in bounds
+                        if (slot >= a.k) { select_broken(a); continue; }  // an inconsistent select: surfaced
                         a.idx[slot] = a.bug_compat ? (uint32_t)slot : (uint32_t)(e + j) + (uint32_t)a.idx_offset;
                         a.val[slot] = comp(v[u], j);
                     }
@@ -530,7 +541,12 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
             a.val[s] = 0.f;
         }
     }
-    if (tile == 0 && tid == 0) *a.count_out = a.cap;
+    // the count, unless a tile already found the select inconsistent (one
+    // finding it later poisons the count itself)
+    if (tile == 0 && tid == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (!(ld_sc1(a.fail) & FAIL_SELECT)) st_sc1(a.count_out, a.cap);
+    }
 }
 
 __global__ void tk_empty(uint32_t *count_out, uint32_t cap) { *count_out = cap; }
@@ -589,6 +605,7 @@ hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s) {
     t.idx = a.idx;
     t.val = a.val;
     t.count_out = a.count_out;
+    t.fail = ws.fail;
     t.rs = ws.rsel;
     t.tile_gt = ws.tile_cnt;
     t.tile_eq = ws.tile_aux;

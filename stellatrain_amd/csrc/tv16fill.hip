@@ -983,12 +983,14 @@ tv16_fill(Tv16FillArgs A) {
     __syncthreads();
     stamp(3);
     count_path(3);
-    full_path(S, d, cnt, N, t, tail, tail_key, A.fail);
-    if (LONE && A.helpers && tid == 0) {  // the literal heap emitted it all: release the helpers
+    // the literal heap emits everything itself: release the helpers before it
+    // runs (an empty share each), so none of them waits out its length
+    if (LONE && A.helpers && tid == 0) {
         st_sc1(&A.cc->pad[2], 0u);
         __builtin_amdgcn_s_waitcnt(0);
         st_sc1(&A.cc->pad[1], ready_tag);
     }
+    full_path(S, d, cnt, N, t, tail, tail_key, A.fail);
     stamp(0);
 }
 

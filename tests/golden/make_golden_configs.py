@@ -19,7 +19,8 @@ generator (stellatrain_amd/synth.py == csrc/synth.hip == orc_synth_fill).
       varies (cnt > cap overflow and cnt < k both occur): counts, threshold
       bits, stream sha256; full idx of call 0.
   C4  the 1,024-bucket stream (shard.c4_sizes), 2 sweeps (the engine's iter%2
-      buffers): per bucket and sweep the count, threshold bits and set sha256.
+      buffers): per bucket and sweep the count, threshold bits, set sha256 and
+      stream sha256 (the regime-B heap fill's pop order, thresholdv16.cpp:261-293).
   C5  64 MiB compress -> MERGE decompress (world 1) -> momentum SGD, 3 steps:
       sha256 of param and momentum after every step.
 
@@ -132,7 +133,7 @@ def c4(ref, o):
             src = gen(o, n, seed_for(b, sw))
             cnt, idx, val = ref.tv16_compress(h, plan.key(b), src, k)
             t, _ = ref.tv16_state(h, plan.key(b))
-            rows.append([sw, b, cnt, tbits(t), set_sha(idx, val, cnt)])
+            rows.append([sw, b, cnt, tbits(t), set_sha(idx, val, cnt), stream_sha(idx, val, cnt)])
         print(f"  c4 sweep {sw} done ({time.time() - t0:.0f} s)", flush=True)
     ref.tv16_free(h)
     return dict(C4, count=len(sizes), sizes_sha=sha(np.array(sizes, np.int64)), rows=rows)

@@ -59,3 +59,16 @@ def line_keys(src: np.ndarray, idx: np.ndarray, oracle) -> np.ndarray:
     lines = np.asarray(idx, np.int64) // 16
     keep = lines < sums.size
     return np.sort(sums[lines[keep]])
+
+
+def assert_topk_values(vg, vo):
+    """Same-cardinality top-k values (topk.cpp:28-46 partition order is free):
+    the SIGNED bit patterns agree as a multiset, except that among exact |x|
+    ties at the k-th magnitude either sign may have been kept."""
+    vg, vo = np.asarray(vg, np.float32), np.asarray(vo, np.float32)
+    assert vg.size == vo.size
+    cut = np.abs(vo).min() if vo.size else np.float32(0)
+    assert np.abs(vg).min() == cut if vg.size else True
+    above_g, above_o = vg[np.abs(vg) > cut], vo[np.abs(vo) > cut]
+    np.testing.assert_array_equal(np.sort(bits(above_g)), np.sort(bits(above_o)))
+    assert np.count_nonzero(np.abs(vg) == cut) == np.count_nonzero(np.abs(vo) == cut)

@@ -148,7 +148,7 @@ def test_cpp_shim_binary_matches_oracle(gpu, oracle, method, tmp_path):
             assert cg == ce
             if method == "topk":
                 np.testing.assert_array_equal(ig, np.arange(k))
-                from test_gpu_codecs import assert_topk_values
+                from parity import assert_topk_values
                 assert_topk_values(vg, ve[:ce])
             else:
                 assert_same_pairs(ig, vg, ie, ve, ce)

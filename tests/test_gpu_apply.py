@@ -18,6 +18,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
+from parity import assert_same_stream
 from stellatrain_amd.synth import D1, D2, seed_for, synth
 
 pytestmark = pytest.mark.gpu
@@ -204,41 +205,49 @@ def test_error_feedback_kernel(gpu, n, off, numel):
 @pytest.mark.parametrize("method", ["thresholdv16", "thresholdv", "topk_exact"])
 def test_merge_compress_batch_error_feedback(gpu, oracle, method):
     """stg_merge_compress_batch_device (compress.cpp:139-186) on a batch with
-    ragged buckets and a repeated key: the (idx, val, count) streams equal the
-    plain codec's, and every bucket and residual end as the bucket with all
-    numel selected slots zeroed.  thresholdv16 takes the fused residual copy."""
+    ragged buckets, a repeated key and one 64 MiB bucket, against the ORACLE
+    replaying the same calls in batch order: every (idx, val) stream and count
+    is the oracle's, and every bucket and residual end as the bucket with the
+    oracle's numel selected slots zeroed (unwritten slots hold index 0,
+    compress.cpp:60-64,178-179).  thresholdv16 takes the fused residual copy."""
     import torch
     from stellatrain_amd import make_compressor
-    sizes = [(1 << 20) + 5, 65536, 100013, 4099, 262144]
-    keys = ["a@w", "b@w", "c@w", "a@w", "d@w"]  # a@w twice: the batch splits its launch
-    comp, ref = make_compressor(method), make_compressor(method)
+    sizes = [(1 << 20) + 5, 65536, 100013, 4099, 262144, 1 << 24]
+    keys = ["a@w", "b@w", "c@w", "a@w", "d@w", "e@w"]  # a@w twice: the batch splits its launch
+    comp = make_compressor(method)
+    h = oracle.tv16_new() if method == "thresholdv16" else oracle.tv_new() if method == "thresholdv" else None
     keep = []  # threshold-v keys its state by src pointer: no pointer reuse across iterations
-    for it in range(2):
-        items, ritems, res, grads, srcs = [], [], [], [], []
+    for it in range(3):
+        items, res, grads, srcs = [], [], [], []
         for j, (n, key) in enumerate(zip(sizes, keys)):
             src = synth(n, seed_for(60 + j, it), D2 if j % 2 else D1)
             k = oracle.merge_numel(n, 0.99)
             g = torch.from_numpy(src.copy()).to(gpu)
             items.append((key, g, k, torch.zeros(k, dtype=torch.int32, device=gpu),
                           torch.zeros(k, dtype=torch.float32, device=gpu)))
-            ritems.append((key, torch.from_numpy(src.copy()).to(gpu), k, torch.zeros(k, dtype=torch.int32, device=gpu),
-                           torch.zeros(k, dtype=torch.float32, device=gpu)))
             res.append(torch.full((n,), 7.0, dtype=torch.float32, device=gpu))
             grads.append(g)
             srcs.append(src)
-        keep.append((items, ritems, res))
-        cnt = comp.compress_batch_async(items, residuals=res)
-        rcnt = ref.compress_batch_async(ritems)
-        torch.cuda.synchronize()
-        assert np.array_equal(cnt.cpu().numpy(), rcnt.cpu().numpy())
-        for j in range(len(items)):
-            ii, rv = items[j][3].cpu().numpy(), ritems[j][4].cpu().numpy()
-            assert np.array_equal(ii, ritems[j][3].cpu().numpy())
-            assert np.array_equal(items[j][4].cpu().numpy().view(np.uint32), rv.view(np.uint32))
-            expect = srcs[j].copy()
-            expect[ii.view(np.uint32)] = 0.0
-            assert np.array_equal(res[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), j
-            assert np.array_equal(grads[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), j
+        keep.append((items, res))
+        cnt = comp.compress_batch_async(items, residuals=res).cpu().numpy()
+        for j, (key, _, k, di, dv) in enumerate(items):
+            src = srcs[j]
+            if method == "thresholdv16":
+                co, io, vo = oracle.tv16_compress(h, key, src, k)
+            elif method == "thresholdv":  # a fresh src pointer every call: a fresh key
+                co, io, vo = oracle.tv_compress(h, 1000 * it + j, src, k)
+            else:
+                co, io, vo = oracle.topk_compress(src, k, bug_compat=False)
+            assert int(cnt[j]) == co, (it, j)
+            ig, vg = di.cpu().numpy().view(np.uint32), dv.cpu().numpy()
+            assert_same_stream(ig, vg, io, vo, co)
+            expect = src.copy()
+            expect[io[:k]] = 0.0  # every one of the numel slots (compress.cpp:178-179)
+            assert np.array_equal(res[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), (it, j)
+            assert np.array_equal(grads[j].cpu().numpy().view(np.uint32), expect.view(np.uint32)), (it, j)
+    comp.check_device()
+    if h is not None:
+        (oracle.tv16_free if method == "thresholdv16" else oracle.tv_free)(h)
 
 
 def test_merge_path_python_api(gpu, oracle):

@@ -10,7 +10,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from parity import assert_same_stream, bits
+from parity import assert_same_stream, assert_topk_values, bits
 from stellatrain_amd.synth import D1, D2, D3, seed_for, synth
 
 pytestmark = pytest.mark.gpu
@@ -154,19 +154,6 @@ def test_topk_bug_compat(gpu, oracle, n, k):
     assert comp.compress("x", torch.from_numpy(src).to(gpu), k, idx, val) == co
     np.testing.assert_array_equal(idx.cpu().numpy(), np.arange(k))
     assert_topk_values(val.cpu().numpy(), vo)
-
-
-def assert_topk_values(vg, vo):
-    """Same-cardinality top-k values (topk.cpp:28-46 partition order is free):
-    the SIGNED bit patterns agree as a multiset, except that among exact |x|
-    ties at the k-th magnitude either sign may have been kept."""
-    vg, vo = np.asarray(vg, np.float32), np.asarray(vo, np.float32)
-    assert vg.size == vo.size
-    cut = np.abs(vo).min() if vo.size else np.float32(0)
-    assert np.abs(vg).min() == cut if vg.size else True
-    above_g, above_o = vg[np.abs(vg) > cut], vo[np.abs(vo) > cut]
-    np.testing.assert_array_equal(np.sort(bits(above_g)), np.sort(bits(above_o)))
-    assert np.count_nonzero(np.abs(vg) == cut) == np.count_nonzero(np.abs(vo) == cut)
 
 
 @pytest.mark.parametrize("n,k,off", [(100013, 1000, 0), (1 << 20, 10485, 77), (4099, 41, 0)])

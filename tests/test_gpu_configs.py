@@ -175,11 +175,12 @@ def test_c4_stream_1024_buckets(gpu):
         torch.cuda.synchronize()
         cn, ih, vh = counts.cpu().numpy(), oidx.cpu().numpy().view(np.uint32), oval.cpu().numpy()
         for b in range(len(sizes)):
-            _, _, cnt, tb, ss = rows[(sw, b)]
+            _, _, cnt, tb, ss, st = rows[(sw, b)]
             t = comp.state(plan.key(b))[0]
-            got = (int(cn[b]), fbits(t), set_sha(ih[koffs[b]:], vh[koffs[b]:], int(cn[b])))
-            if got != (cnt, tb, ss):
-                bad.append((sw, b, got[:2], (cnt, tb)))
+            got = (int(cn[b]), fbits(t), set_sha(ih[koffs[b]:], vh[koffs[b]:], int(cn[b])),
+                   stream_sha(ih[koffs[b]:], vh[koffs[b]:], int(cn[b])))
+            if got != (cnt, tb, ss, st):  # the stream too: the heap fill's pop order (thresholdv16.cpp:261-293)
+                bad.append((sw, b, got[:2], (cnt, tb), got[2] == ss, got[3] == st))
     comp.check_device()
     assert not bad, bad[:8]
 
