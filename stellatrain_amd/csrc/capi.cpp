@@ -54,7 +54,7 @@ struct Workspace {
     std::mutex mu;
     stg::DevWS d{};
     void *fixed = nullptr;
-    size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0, cap_desc = 0;
+    size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0, cap_desc = 0, cap_lone = 0;
     uint32_t epoch = 0;  // thresholdv16 call counter (hand-off tags)
     // threshold-v: the ticket's value at the next call, the last call's
     // range-descriptor tag and the descriptor block last zeroed (tile_cnt, its size)
@@ -81,6 +81,10 @@ struct Workspace {
         (void)hipFree(d.tile_aux);
         (void)hipFree(d.stage_pos);
         (void)hipFree(d.stage_val);
+        (void)hipFree(d.ldesc);
+        (void)hipFree(d.lq);
+        (void)hipFree(d.lw);
+        (void)hipFree(d.lv);
         (void)hipFree(h_src);
         (void)hipFree(h_idx);
         (void)hipFree(h_val);
@@ -138,6 +142,29 @@ struct Workspace {
         int rc;
         if ((rc = grow(d.desc, cap_desc, n))) return rc;
         HIP_TRY(hipMemsetAsync(d.desc, 0, cap_desc * sizeof(stg::ChunkDesc), stream));
+        return STG_OK;
+    }
+
+    // one-bucket path lists (tv16lone.hip): per chunk a count pair and the
+    // qualifying / window line lists; written before they are read in every call
+    int ensure_lone(size_t nc) {
+        if (nc <= cap_lone) return STG_OK;
+        HIP_TRY(hipStreamSynchronize(stream));
+        (void)hipFree(d.ldesc);
+        (void)hipFree(d.lq);
+        (void)hipFree(d.lw);
+        (void)hipFree(d.lv);
+        d.ldesc = nullptr;
+        d.lq = nullptr;
+        d.lw = nullptr;
+        d.lv = nullptr;
+        const size_t c = std::min<size_t>(stg::LMAXC, std::max(nc, cap_lone + cap_lone / 2));
+        cap_lone = 0;
+        HIP_TRY(hipMalloc(&d.ldesc, c * sizeof(uint2)));
+        HIP_TRY(hipMalloc(&d.lq, c * stg::LQCAP * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&d.lw, c * stg::LWCAP * sizeof(uint4)));
+        HIP_TRY(hipMalloc(&d.lv, c * stg::LQCAP * 4 * sizeof(float4)));
+        cap_lone = c;
         return STG_OK;
     }
 
@@ -355,6 +382,10 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
         chunks += std::max<size_t>(1, (b.n / 16 + stg::TV16_CHUNK - 1) / stg::TV16_CHUNK);
     }
     if ((rc = ws->ensure_desc(chunks))) return rc;
+    if (grp.size() == 1) {  // the one-bucket path's lists (tv16lone.hip), in its own chunks
+        const size_t lc = std::max<size_t>(1, (grp[0].n / 16 + stg::LCHUNK - 1) / stg::LCHUNK);
+        if (lc <= stg::LMAXC && (rc = ws->ensure_lone(lc))) return rc;
+    }
     std::array<hipEvent_t, 3> evs{};
     bool timed = false;
     if ((rc = h->take_events(&evs, &timed))) return rc;
@@ -384,6 +415,7 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / inflight * XCDS)
                      : (uint32_t)(2 * h->num_cu);
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
+    a.lone_cap = (uint32_t)ws->cap_lone;
     FusedLane &lane = g_lanes[h->device & 63];
     std::lock_guard<std::mutex> lg(lane.mu);
     const size_t max_inflight = inflight;

@@ -788,6 +788,61 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
     static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
     const bool lone_scan = lone_ok && a.nb == 1;
+    // the one-bucket path: a scan with no waits between workgroups, finished
+    // by the fill launch (tv16lone.hip; STG_TV16_LFIN=0: the batched scan)
+    static const bool lfin_ok = !(getenv("STG_TV16_LFIN") && atoi(getenv("STG_TV16_LFIN")) == 0);
+    const uint32_t KL = std::max<uint32_t>(1, (A.bk[0].nb + LCHUNK - 1) / LCHUNK);  // one-bucket chunks
+    if (lone_scan && lfin_ok && !dbg_stage && KL <= a.lone_cap && KL <= LMAXC && ws.ldesc) {
+        if (a.ev) (void)hipEventRecord(a.ev[0], s);
+        LScanArgs L{};
+        L.src = a.b[0].src;
+        L.nb = A.bk[0].nb;
+        L.nc = KL;
+        L.state = a.b[0].state;
+        L.cp = ws.cp;
+        L.resid = a.b[0].resid;
+        L.ldesc = ws.ldesc;
+        L.lq = ws.lq;
+        L.lw = ws.lw;
+        L.lv = ws.lv;
+        L.zero_next = reinterpret_cast<uint32_t *>(&ws.ctl->cc[(a.epoch + 1) & 1u]);
+        hipError_t e = launch_tv16_lscan(L, a.num_cu, s);
+        if (e != hipSuccess) return e;
+        if (a.ev) (void)hipEventRecord(a.ev[1], s);
+        if (a.scan_done && (e = hipEventRecord(a.scan_done, s)) != hipSuccess) return e;
+        F.nbk = 1;
+        F.epoch = a.epoch;
+        F.dec = ws.ctl->dec;
+        F.fail = ws.fail;
+        F.dbg = ws.misc;
+        static const uint32_t fill_mode =
+            getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
+        F.mode = fill_mode;
+        F.lone = true;
+        static const uint32_t helpers =
+            getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
+        static const uint32_t workers = std::max(1, std::min(
+            getenv("STG_TV16_LFIN_WORKERS") ? atoi(getenv("STG_TV16_LFIN_WORKERS")) : 64, 192));
+        (void)helpers;
+        static const uint32_t rankers = std::max(0, std::min(
+            getenv("STG_TV16_LFIN_RANKERS") ? atoi(getenv("STG_TV16_LFIN_RANKERS")) : 32, 128));
+        F.helpers = 0;
+        F.cc = &ws.ctl->cc[a.epoch & 1u];
+        F.lfin = true;
+        F.workers = workers;
+        F.rankers = rankers;
+        F.nc = KL;
+        F.ldesc = ws.ldesc;
+        F.lq = ws.lq;
+        F.lw = ws.lw;
+        F.lv = ws.lv;
+        F.state = a.b[0].state;
+        F.cp = ws.cp;
+        F.resid = a.b[0].resid;
+        if ((e = launch_tv16_fill(F, s)) != hipSuccess) return e;
+        if (a.ev) (void)hipEventRecord(a.ev[2], s);
+        return hipGetLastError();
+    }
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     switch (dbg_stage) {
         case 1: tv16_batch<1, false, false><<<G, FWG, 0, s>>>(A); break;

@@ -380,6 +380,8 @@ __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uin
     emit_order(d, cnt, rem, np, tail_rank, [&](uint32_t i) { return hld(H, N - 1 - i).y; });
 }
 
+#include "tv16lfin.h"
+
 #ifndef STG_FILL_STAMPS
 #define STG_FILL_STAMPS 0
 #endif
@@ -398,13 +400,58 @@ tv16_fill(Tv16FillArgs A) {
     // LONE with helpers: one bucket, 1 + A.helpers workgroups; the first to
     // start (ticket 0) orders the lines, the others wait for its order and
     // emit a share of it (each waits only on a workgroup already running)
-    __shared__ uint32_t s_role;
+    __shared__ uint32_t s_role, s_last;
     const uint32_t tid = threadIdx.x;
     uint32_t role = 0;
-    if (LONE && A.helpers) {
+    if (LONE && (A.helpers || A.lfin)) {
         if (tid == 0) s_role = g_add(&A.cc->pad[0], 1u);
         __syncthreads();
         role = s_role;
+    }
+    // lfin (tv16lfin.h): tickets [0, workers) finish the scan, the next
+    // `rankers` order the regime-B fill in parallel; the last workgroup to
+    // finish runs the exact orderer below only when the rankers could not
+    // prove their order.  No helpers in this mode.
+    const uint32_t first_helper = A.lfin ? 0xffffffffu : 1u;
+    if (LONE && A.lfin) {
+        LfinLds &Lf = *reinterpret_cast<LfinLds *>(fill_lds);
+        if (tid == 0) {
+            LfinArgs &W = Lf.args;
+            W.d = A.bk[0];
+            W.nc = A.nc;
+            W.workers = A.workers;
+            W.rankers = A.rankers;
+            W.epoch = A.epoch;
+            W.mode = A.mode;
+            W.ldesc = A.ldesc;
+            W.lq = A.lq;
+            W.lw = A.lw;
+            W.lv = A.lv;
+            W.state = A.state;
+            W.cp = A.cp;
+            W.resid = A.resid;
+            W.fail = A.fail;
+            W.dec = const_cast<Decision *>(A.dec);
+            W.cc = A.cc;
+            W.dbg = A.dbg;
+        }
+        __syncthreads();
+        if (role < A.workers) lfin_worker(Lf, role);
+        else if (role < A.workers + A.rankers) lfin_ranker(Lf, role - A.workers);
+        vm_drain();  // every wave's stores drained, then one add for the workgroup
+        __syncthreads();
+        if (tid == 0) s_last = g_add(&A.cc->pad[4], 1u) == A.workers + A.rankers - 1;
+        __syncthreads();
+        if (!s_last) return;
+        const uint32_t rep = ld_sc1(&A.cc->pad[5]);
+        // how the call's fill was ordered (debug words 48..51: rankers without
+        // ties, rankers with ties, the orderer after a violation, the orderer
+        // for a call the rankers could not take; tests read them)
+        const bool ranked = A.rankers && !(rep & LF_FALLBACK) && !((rep & LF_TIES) && (rep & LF_VIOL));
+        if (tid == 0 && (rep & (LF_RANKED | LF_FALLBACK)))
+            atomicAdd(&A.dbg[48 + (ranked ? ((rep & LF_TIES) ? 1 : 0) : ((rep & LF_FALLBACK) ? 3 : 2))], 1u);
+        if (ranked) return;
+        __syncthreads();  // the orderer's LDS view goes over the lfin view
     }
     const uint32_t b = LONE ? 0u : blockIdx.x;  // a lone launch has one bucket
     uint32_t nst = 0;
@@ -423,10 +470,23 @@ tv16_fill(Tv16FillArgs A) {
     const Decision &D = A.dec[b];
     uint32_t *const order_g = const_cast<uint32_t *>(d.cand) + 3 * CAND_CAP;  // the spare window array: the order
     const uint32_t ready_tag = (A.epoch << 8) | 0x5au;
-    if (LONE && role) {  // a helper: wait for the orderer's pop order, emit share `role` of it
-        const uint64_t h0 = ld_sc1(&D.w[0]), h1 = ld_sc1(&D.w[1]);
+    if (LONE && role >= first_helper) {  // a helper: wait for the orderer's pop order, emit share `role` of it
+        const uint32_t share = role - first_helper + 1;
+        uint64_t h0 = ld_sc1(&D.w[0]);
+        if (A.lfin) {  // the decision comes from worker 0 of this launch (ticket 0: running)
+            uint64_t st1 = 0;
+            for (uint32_t spins = 0; (uint32_t)(h0 >> 32) != ((A.epoch << 8) | TV16_TAG_DEC); ++spins) {
+                __builtin_amdgcn_s_sleep(4);
+                h0 = ld_sc1(&D.w[0]);
+                if (spin_expired(spins, st1)) {
+                    if (tid == 0) { g_or(A.fail, FAIL_SPIN_TIMEOUT); st_sc1(d.count_out, POISON_COUNT); }
+                    return;
+                }
+            }
+        }
+        const uint64_t h1 = ld_sc1(&D.w[1]);
         if ((uint32_t)(h0 >> 32) != ((A.epoch << 8) | TV16_TAG_DEC) || !((uint32_t)h0 & TV16_DEC_B) ||
-            ld_sc1(A.fail) || role > A.helpers)
+            ld_sc1(A.fail) || share > A.helpers)
             return;  // no regime-B fill (or the scan failed): nothing to emit
         if (!(uint32_t)h1 && !((uint32_t)h0 & TV16_DEC_TAIL)) return;  // nothing missing (the orderer returns too)
         uint64_t st0 = 0;
@@ -449,8 +509,8 @@ tv16_fill(Tv16FillArgs A) {
         const uint32_t tl = d.tl, ioff = (uint32_t)d.idx_offset;
         const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(oidx) |
                            reinterpret_cast<uintptr_t>(oval)) & 15u) == 0 && (cnt & 3u) == 0;
-        const uint32_t i1 = min(P, (role + 1) * chunk), q = tid & 3u;
-        for (uint32_t i = role * chunk + (tid >> 2); i < i1; i += FILL_WG / 4) {
+        const uint32_t i1 = min(P, (share + 1) * chunk), q = tid & 3u;
+        for (uint32_t i = share * chunk + (tid >> 2); i < i1; i += FILL_WG / 4) {
             const uint32_t o16 = 16u * i - (tail_rank < i ? 16u - tl : 0u);
             if (o16 >= rem) continue;
             const uint32_t len = min(i == tail_rank ? tl : 16u, rem - o16);
@@ -996,6 +1056,9 @@ tv16_fill(Tv16FillArgs A) {
 
 }  // namespace
 
+constexpr size_t LFIN_LDS = sizeof(FillLds) > sizeof(LfinLds) ? sizeof(FillLds) : sizeof(LfinLds);
+static_assert(LFIN_LDS <= 160 * 1024, "one lfin workgroup per CU");
+
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {
     if (!a.nbk) return hipSuccess;
     static const hipError_t attr0 =
@@ -1003,10 +1066,11 @@ hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {
                             (int)sizeof(FillLds));
     static const hipError_t attr1 =
         hipFuncSetAttribute(reinterpret_cast<const void *>(&tv16_fill<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(FillLds));
+                            (int)LFIN_LDS);
     if (attr0 != hipSuccess) return attr0;
     if (attr1 != hipSuccess) return attr1;
-    if (a.lone) tv16_fill<true><<<a.nbk + a.helpers, FILL_WG, sizeof(FillLds), s>>>(a);
+    if (a.lfin) tv16_fill<true><<<a.workers + a.rankers, FILL_WG, LFIN_LDS, s>>>(a);
+    else if (a.lone) tv16_fill<true><<<a.nbk + a.helpers, FILL_WG, sizeof(FillLds), s>>>(a);
     else tv16_fill<false><<<a.nbk, FILL_WG, sizeof(FillLds), s>>>(a);
     return hipGetLastError();
 }

@@ -1,0 +1,565 @@
+// tv16lfin.h -- the finish of a one-bucket thresholdv16 scan (tv16lone.hip),
+// inside the fill launch (tv16fill.hip, lfin mode).  Included by tv16fill.hip
+// in its anonymous namespace, after FillLds and the fill's helpers.
+//
+// Reference: ThresholdvCompressor16::impl_simd_v2 after the streaming
+// (thresholdv16.cpp:138-259: emission order, stage 2's partial line, stage 3's
+// ragged tail, AIMD) and the regime-B heap fill (:261-293).
+//
+// The scan left per chunk of LCHUNK lines its counts (ldesc), its qualifying
+// lines in order with their data (lq, lv) and its window lines in order (lw).
+// Three roles share the launch, none waits on another:
+//   workers  (tickets [0, workers))  take the chunks' prefix counts, decide
+//            the regime exactly as the batched scan's last chunk does
+//            (tv16.hip finish_chunk), write a balanced share of the
+//            qualifying lines at their global ranks and of the window list in
+//            scan order (the exact orderer's input); worker 0 writes the
+//            ragged tail, the AIMD state, the count and the decision;
+//   rankers  (the next `rankers` tickets)  decide the same way; in regime B
+//            each loads the whole window list, keeps the top bins (the pops,
+//            the first line past them and its ties), ranks a balanced share
+//            of the kept lines by (sum desc, right-first pre-order of the
+//            start position) -- the pop order whenever the fill's fast paths
+//            hold (see tv16fill.hip (2), (3)) -- and writes them; it checks
+//            those conditions for its share and reports ties / violations;
+//   every workgroup then adds to one counter; the last one (every write of
+//            the others is in) runs the exact orderer of tv16fill.hip over the
+//            workers' window list when the rankers could not prove their
+//            order (a violation among ties, a window the scan's lists could
+//            not hold, or the window missed the top), overwriting the fill.
+#pragma once
+
+// LDS of the lfin roles (a view of the launch's dynamic LDS, like FillLds).
+struct LfinArgs {
+    Tv16FillBucket d;
+    uint32_t nc, workers, rankers, epoch, mode;
+    const uint2 *ldesc;
+    const uint32_t *lq;
+    const uint4 *lw;
+    const float4 *lv;
+    KeyState *state;
+    const CallParams *cp;
+    float *resid;
+    uint32_t *fail;
+    Decision *dec;
+    CallCtl *cc;
+    uint32_t *dbg;  // diagnostics: lfin counters at words 48..55, ranker 0's phase stamps at 32..47
+};
+constexpr uint32_t LF_QMAP = 8192;  // worker: ranks mapped to their chunk per pass
+struct LfinLds {
+    uint32_t qp[LMAXC + 1];  // per chunk: exclusive prefix of qualifying lines (+ total)
+    uint32_t wp[LMAXC + 1];  // ... of window lines
+    union {
+        struct {               // ranker: the window, by entry (scan order)
+            uint32_t key[CAND_CAP + 1];  // order key ford(line sum); the ragged tail last
+            uint32_t cix[CAND_CAP + 1];  // candidate index = the line's start heap position
+            uint32_t lin[CAND_CAP + 1];  // line (the tail: nb); first the entry's chunk
+        } r;
+        struct {               // worker: rank -> chunk
+            uint16_t qmap[LF_QMAP];
+        } w;
+    } u;
+    uint32_t bin[NBIN];        // ranker: window histogram -> bin starts
+    uint32_t sh[32];
+    uint32_t bl[64];           // the bin holding rank pc: its kept entries
+    uint32_t rcnt[64];         // rank partial counts of the current group of 64 entries
+    uint32_t cut, wk, nbl, tail_e, tail_rank, kh, flags;
+    LfinArgs args;
+};
+// the kept lines, compacted: keys and candidate indices over qp / wp (no
+// longer read by then), lines in place over the window's lines
+static_assert(2 * EMAX * sizeof(uint32_t) <= 2 * (LMAXC + 1) * sizeof(uint32_t), "kept lines fit over the prefixes");
+
+__device__ __forceinline__ uint32_t chunk_of(const uint32_t *p, uint32_t nc, uint32_t g) {
+    uint32_t lo = 0, hi = nc;  // the last c < nc with p[c] <= g (p ascending, p[0] = 0)
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (p[m] <= g) lo = m; else hi = m;
+    }
+    return lo;
+}
+
+// ranker report bits (CallCtl pad[5])
+constexpr uint32_t LF_TIES = 1u;      // equal sums among the first pops + 1
+constexpr uint32_t LF_VIOL = 2u;      // a fast-path condition failed for a tied or late line
+constexpr uint32_t LF_FALLBACK = 4u;  // the rankers could not order this call at all
+constexpr uint32_t LF_RANKED = 8u;    // a regime-B call the rankers took
+
+#ifndef STG_FILL_STAMPS
+#define STG_FILL_STAMPS 0
+#endif
+// diagnostics (STG_FILL_STAMPS builds): ranker 0's phase stamps, words 32..47
+#define LF_STAMP(i)                                                                                  \
+    do {                                                                                             \
+        if (STG_FILL_STAMPS && rk == 0 && threadIdx.x == 0)                                          \
+            A.dbg[32 + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime();                            \
+    } while (0)
+
+// What every lfin workgroup decides, identically.
+struct LfinDec {
+    uint32_t Qtot, Wtot, kb, r, lim, c0, ct, cnt, M, N;
+    bool regimeB, tail_cand, listw, lists_ok;
+    float t, inc, tail_key;
+};
+
+// Per-chunk counts -> exclusive prefixes in LDS, and the regime decision of
+// tv16.hip finish_chunk (thresholdv16.cpp:138-259).
+__device__ __forceinline__ void lfin_prefix(LfinLds &L, const LfinArgs &A, LfinDec &D) {
+    const Tv16FillBucket &d = A.d;
+    const uint32_t tid = threadIdx.x, nc = A.nc;
+    constexpr uint32_t PER = LMAXC / FILL_WG;
+    static_assert(PER * FILL_WG == LMAXC, "chunks per thread");
+    // the ragged tail's floats, loaded with the counts (one round trip)
+    float tv[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) tv[i] = i < d.tl ? d.src[(size_t)d.nb * 16 + i] : 0.f;
+    uint32_t qv[PER], wv[PER], sq = 0, sw = 0, bad = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t c = tid * PER + u;
+        const uint2 x = c < nc ? A.ldesc[c] : make_uint2(0u, 0u);
+        qv[u] = x.x;
+        wv[u] = x.y;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) {
+        sq += qv[u];
+        sw += wv[u];
+        bad |= (qv[u] > LQCAP || wv[u] > LWCAP) ? 1u : 0u;
+    }
+    D.t = A.cp->t;
+    D.inc = A.cp->inc;
+    uint32_t pq = blk_excl_scan<FNW_F>(sq, L.sh, &D.Qtot);
+    uint32_t pw = blk_excl_scan<FNW_F>(sw, L.sh, &D.Wtot);
+#pragma unroll
+    for (uint32_t u = 0; u < PER; ++u) {
+        const uint32_t c = tid * PER + u;
+        if (c < nc) { L.qp[c] = pq; L.wp[c] = pw; }
+        pq += qv[u];
+        pw += wv[u];
+    }
+    if (tid == 0) { L.qp[nc] = D.Qtot; L.wp[nc] = D.Wtot; }
+    D.lists_ok = !__syncthreads_or((int)bad);
+    const uint32_t Qtot = D.Qtot;
+    D.kb = d.dst_len / 16;
+    D.r = d.dst_len % 16;
+    D.lim = D.kb + (D.r ? 1u : 0u);
+    D.c0 = Qtot >= D.lim ? d.dst_len : 16u * Qtot;
+    D.tail_cand = false;
+    D.tail_key = 0.f;
+    D.ct = 0;
+    if (D.c0 < d.dst_len && d.tl) {  // stage 3: the ragged tail's signed, sequential sum (thresholdv16.cpp:212-236)
+        float sm = 0.f;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i)
+            if (i < d.tl) sm += tv[i];
+        if (sm * 16.0f >= D.t * (float)d.tl) D.ct = min(d.dst_len - D.c0, d.tl);
+        else { D.tail_cand = true; D.tail_key = sm * 16.0f / (float)d.tl; }
+    }
+    D.cnt = D.c0 + D.ct;
+    D.regimeB = D.cnt < d.dst_len;
+    const uint32_t ncand = d.nb - Qtot;  // non-qualifying full lines
+    D.M = D.regimeB ? min((d.dst_len - D.cnt + 15u) / 16u, ncand) : 0u;
+    D.listw = D.regimeB && D.Wtot >= D.M && D.Wtot + 1 <= CAND_CAP;
+    D.N = ncand + (D.tail_cand ? 1u : 0u);  // the reference's candidate vector length
+}
+
+// A chunk whose lists overflowed, read again from src by one workgroup, in
+// order: its qualifying lines (emitted at their ranks) and window lines.
+__device__ __forceinline__ void lfin_rescan(LfinLds &L, const Tv16FillBucket &d, uint32_t c, const LfinDec &D,
+                                            bool emit, bool list) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t L0 = c * LCHUNK;
+    const uint32_t nl = d.nb > L0 ? min(LCHUNK, d.nb - L0) : 0u;
+    const uint32_t tb = f2u(D.t), wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
+    const bool vec = aligned16(d);
+    uint32_t *cu = const_cast<uint32_t *>(d.cand), *cl = cu + CAND_CAP, *ci = cu + 2 * CAND_CAP;
+    uint32_t qb = L.qp[c], wb = L.wp[c];
+    for (uint32_t l0 = 0; l0 < nl; l0 += FILL_WG) {
+        const uint32_t l = l0 + tid;
+        const float sm = l < nl ? lane_line_sum(d.src + (size_t)(L0 + l) * 16) : 0.f;
+        const uint32_t u = f2u(sm);
+        const bool qf = l < nl && sm >= D.t;
+        const bool wf = l < nl && u >= wlo && u < tb;
+        uint32_t tq, tw;
+        const uint32_t rq = blk_excl_scan<FNW_F>(qf ? 1u : 0u, L.sh, &tq);
+        const uint32_t rw = blk_excl_scan<FNW_F>(wf ? 1u : 0u, L.sh, &tw);
+        if (emit && qf && qb + rq < D.lim) {
+            const uint32_t g = qb + rq;
+            emit_line(d, vec, (L0 + l) * 16, 16 * g, g == D.kb ? D.r : 16u);
+        }
+        if (list && wf && wb + rw < CAND_CAP) {
+            st_sc1(&cu[wb + rw], u);
+            st_sc1(&cl[wb + rw], (L0 + l) * 16);
+            st_sc1(&ci[wb + rw], L0 + l - (qb + rq));
+        }
+        qb += tq;
+        wb += tw;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// worker `wk`
+// ---------------------------------------------------------------------------
+__device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
+    const LfinArgs &A = L.args;
+    const Tv16FillBucket &d = A.d;
+    const uint32_t tid = threadIdx.x, nc = A.nc, nwk = A.workers;
+    LfinDec D;
+    lfin_prefix(L, A, D);
+    const uint32_t *qp = L.qp, *wp = L.wp;
+    const bool vec = aligned16(d);
+    // ---- this worker's share of the qualifying lines, by global rank; a map
+    //      rank -> chunk built by one thread per chunk, then every line's two
+    //      loads (its position, its staged data) in flight together ----
+    const uint32_t nq = min(D.Qtot, D.lim);
+    const uint32_t per = (nq + nwk - 1) / nwk, g0 = min(nq, wk * per), g1 = min(nq, g0 + per);
+    for (uint32_t p0 = g0; p0 < g1; p0 += LF_QMAP) {
+        const uint32_t p1 = min(g1, p0 + LF_QMAP);
+        const uint32_t ca = chunk_of(qp, nc, p0), cb = chunk_of(qp, nc, p1 - 1);
+        for (uint32_t c = ca + tid; c <= cb; c += FILL_WG) {
+            const uint32_t a = max(qp[c], p0), b = min(qp[c + 1], p1);
+            for (uint32_t g = a; g < b; ++g) L.u.w.qmap[g - p0] = (uint16_t)c;
+        }
+        __syncthreads();
+        const uint32_t q = tid & 3u;
+        constexpr uint32_t KQ = 4;  // rounds of lines in flight together
+        for (uint32_t gb = p0 + (tid >> 2); gb < p1; gb += KQ * (FILL_WG / 4)) {
+            uint32_t pos[KQ], g[KQ];
+            float4 x[KQ];
+#pragma unroll
+            for (uint32_t k = 0; k < KQ; ++k) {
+                g[k] = gb + k * (FILL_WG / 4);
+                pos[k] = NONE;
+                if (g[k] < p1) {
+                    const uint32_t c = L.u.w.qmap[g[k] - p0], rr = g[k] - qp[c];
+                    if (qp[c + 1] - qp[c] <= LQCAP) {  // an overflowed chunk is re-read below
+                        pos[k] = (c * LCHUNK + A.lq[(size_t)c * LQCAP + rr]) * 16 + 4 * q;
+                        x[k] = A.lv[((size_t)c * LQCAP + rr) * 4 + q];
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < KQ; ++k) {
+                if (pos[k] == NONE) continue;
+                const uint32_t len = g[k] == D.kb ? D.r : 16u, off = 16 * g[k] + 4 * q;
+                const uint32_t bi = pos[k] + (uint32_t)d.idx_offset;
+                if (vec && len == 16) {
+                    *reinterpret_cast<float4 *>(d.val + off) = x[k];
+                    *reinterpret_cast<uint4 *>(d.idx + off) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                } else {
+                    const float xs[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+#pragma unroll
+                    for (uint32_t cc = 0; cc < 4; ++cc)
+                        if (4 * q + cc < len) {
+                            d.val[off + cc] = xs[cc];
+                            d.idx[off + cc] = bi + cc;
+                        }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // ---- regime B: this worker's share of the window list, in scan order
+    //      (the exact orderer's input), one thread per (chunk, slot) ----
+    uint32_t *cu = const_cast<uint32_t *>(d.cand), *cl = cu + CAND_CAP, *ci = cu + 2 * CAND_CAP;
+    const uint32_t pc = (nc + nwk - 1) / nwk, c_lo = min(nc, wk * pc), c_hi = min(nc, c_lo + pc);
+    if (D.listw) {
+        for (uint32_t p = tid; p < (c_hi - c_lo) * LWCAP; p += FILL_WG) {
+            const uint32_t c = c_lo + p / LWCAP, i = p % LWCAP;
+            const uint32_t wc = wp[c + 1] - wp[c];
+            if (i >= wc || wc > LWCAP || qp[c + 1] - qp[c] > LQCAP) continue;  // overflowed: re-read below
+            const uint4 x = A.lw[(size_t)c * LWCAP + i];
+            const uint32_t line = c * LCHUNK + x.y, e = wp[c] + i;
+            st_sc1(&cu[e], x.x);
+            st_sc1(&cl[e], line * 16);
+            st_sc1(&ci[e], line - (qp[c] + x.z));
+        }
+    }
+    // ---- this worker's chunks whose lists overflowed: read again ----
+    if (!D.lists_ok) {
+        for (uint32_t c = c_lo; c < c_hi; ++c) {
+            const uint32_t qc = qp[c + 1] - qp[c], wc = wp[c + 1] - wp[c];
+            const bool emit = qc > LQCAP && qp[c] < D.lim;
+            const bool list = D.listw && wc && (wc > LWCAP || qc > LQCAP);
+            if (emit || list) lfin_rescan(L, d, c, D, emit, list);
+        }
+    }
+    // ---- worker 0: tail, AIMD state, count, decision (tv16.hip finish_chunk) ----
+    if (wk == 0 && tid == 0) {
+        if (D.ct) {
+            const size_t p0 = (size_t)d.nb * 16;
+            for (uint32_t i = 0; i < D.ct; ++i) {
+                d.val[D.c0 + i] = d.src[p0 + i];
+                d.idx[D.c0 + i] = (uint32_t)(p0 + i) + (uint32_t)d.idx_offset;
+            }
+        }
+        if (A.resid && d.tl)  // fused error feedback: the ragged tail is not streamed
+            for (uint32_t i = 0; i < d.tl; ++i) A.resid[(size_t)d.nb * 16 + i] = d.src[(size_t)d.nb * 16 + i];
+        A.state->t = D.regimeB ? (float)((double)D.t * 0.99) : D.t + D.inc;  // thresholdv16.cpp:243-259
+        A.state->inc = D.inc;
+        A.state->init = 1;
+        st_sc1(d.count_out, (uint32_t)min((uint64_t)d.dst_len, (uint64_t)d.nb * 16 + d.tl));
+        if (ld_sc1(A.fail)) st_sc1(d.count_out, POISON_COUNT);
+        uint32_t flags = 0;
+        if (D.regimeB) flags = TV16_DEC_B | (D.tail_cand ? TV16_DEC_TAIL : 0u) | (D.listw ? TV16_DEC_WIN : 0u);
+        Decision &Dc = A.dec[0];
+        st_sc1(&Dc.w[1], ((uint64_t)D.cnt << 32) | D.M);
+        st_sc1(&Dc.w[2], ((uint64_t)D.Wtot << 32) | __float_as_uint(D.tail_key));
+        st_sc1(&Dc.w[3], ((uint64_t)D.Qtot << 32) | __float_as_uint(D.t));
+        vm_drain();
+        st_sc1(&Dc.w[0], ((uint64_t)((A.epoch << 8) | TV16_TAG_DEC) << 32) | flags);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ranker `rk`: the regime-B fill's order for a share of the kept lines
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool is_desc(uint32_t q, uint32_t qt) {  // heap node q (pos + 1) below node qt
+    const uint32_t dp = depth_of(q), dt = depth_of(qt);
+    return dp > dt && (q >> (dp - dt)) == qt;
+}
+
+__device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
+    const LfinArgs &A = L.args;
+    const Tv16FillBucket &d = A.d;
+    const uint32_t tid = threadIdx.x, nc = A.nc;
+    LfinDec D;
+    LF_STAMP(0);
+    if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[42] = (uint32_t)__builtin_amdgcn_s_memtime();  // the shader clock
+    lfin_prefix(L, A, D);
+    LF_STAMP(1);
+    if (!D.regimeB || (!D.M && !D.tail_cand)) return;  // nothing to fill
+    if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_RANKED);
+    const uint32_t tb = f2u(D.t), wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
+    const bool tail_in = D.tail_cand && D.tail_key >= u2f(wlo);
+    const uint32_t W = D.Wtot + (tail_in ? 1u : 0u);
+    if (!D.listw || !D.lists_ok || D.N > POS_LIM || W == 0 || A.mode) {
+        if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+        return;
+    }
+    // ---- the window in LDS: entry -> chunk (one thread per chunk), then
+    //      every entry's load in flight together ----
+    uint32_t *const key = L.u.r.key, *const cix = L.u.r.cix, *const lin = L.u.r.lin;
+    for (uint32_t c = tid; c < nc; c += FILL_WG)
+        for (uint32_t e = L.wp[c]; e < L.wp[c + 1]; ++e) lin[e] = c;
+    __syncthreads();
+    constexpr uint32_t KW = 8;
+    for (uint32_t e0 = tid; e0 < D.Wtot; e0 += KW * FILL_WG) {
+        uint4 x[KW];
+        uint32_t c[KW];
+#pragma unroll
+        for (uint32_t k = 0; k < KW; ++k) {
+            const uint32_t e = e0 + k * FILL_WG;
+            if (e < D.Wtot) {
+                c[k] = lin[e];
+                x[k] = A.lw[(size_t)c[k] * LWCAP + (e - L.wp[c[k]])];
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KW; ++k) {
+            const uint32_t e = e0 + k * FILL_WG;
+            if (e < D.Wtot) {
+                const uint32_t line = c[k] * LCHUNK + x[k].y;
+                key[e] = ford(u2f(x[k].x));
+                cix[e] = line - (L.qp[c[k]] + x[k].z);
+                lin[e] = line;
+            }
+        }
+    }
+    LF_STAMP(2);
+    if (tail_in && tid == 0) {  // the ragged tail: the candidate vector's last entry (thresholdv16.cpp:229-234)
+        key[D.Wtot] = ford(D.tail_key);
+        cix[D.Wtot] = D.N - 1;
+        lin[D.Wtot] = d.nb;
+    }
+    // ---- histogram of 256-ulp bins below t (sum descending); keep the first
+    //      bins holding M + 2 entries: every pop, the first line past them and
+    //      its ties (a bin never splits equal sums) ----
+    for (uint32_t i = tid; i < NBIN; i += FILL_WG) L.bin[i] = 0;
+    __syncthreads();
+    auto kbin = [&](uint32_t ok) -> uint32_t {  // ok = ford(sum)
+        const float k = u2f(ok & 0x80000000u ? ok & 0x7fffffffu : ~ok);
+        if (k >= D.t) return 0u;
+        if (!(k > 0.f)) return NBIN - 1;
+        return min((tb - 1u - f2u(k)) >> 8, NBIN - 1);
+    };
+    for (uint32_t e = tid; e < W; e += FILL_WG) atomicAdd(&L.bin[kbin(key[e])], 1u);
+    __syncthreads();
+    {
+        constexpr uint32_t PER = NBIN / FILL_WG;
+        static_assert(PER == 2, "two bins per thread");
+        const uint32_t b0 = L.bin[PER * tid], b1 = L.bin[PER * tid + 1], need = D.M + 2;
+        uint32_t tot;
+        const uint32_t run = blk_excl_scan<FNW_F>(b0 + b1, L.sh, &tot);
+        L.bin[PER * tid] = run;
+        L.bin[PER * tid + 1] = run + b0;
+        if (run < need && run + b0 >= need) { L.cut = PER * tid + 1; L.wk = run + b0; }
+        else if (run + b0 < need && run + b0 + b1 >= need) { L.cut = PER * tid + 2; L.wk = run + b0 + b1; }
+        if (tid == 0 && tot < need) { L.cut = NBIN; L.wk = tot; }
+        if (tid == 0) { L.tail_e = NONE; L.nbl = 0; L.flags = 0; }
+        __syncthreads();
+    }
+    LF_STAMP(3);
+    const uint32_t cut = L.cut, Wk = L.wk;
+    const uint32_t rem = d.dst_len - D.cnt;
+    const uint32_t covered = 16u * Wk;  // less 16 - tl if the tail is kept (checked below)
+    if (Wk > EMAX || Wk == 0 || covered < rem) {
+        if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+        return;
+    }
+    // ---- the kept lines, compacted (over qp / wp) in entry order ----
+    uint32_t *const kk = L.qp, *const kc = L.qp + EMAX, *const kl = lin;
+    {
+        constexpr uint32_t PE = CAND_CAP / FILL_WG + 1;
+        uint32_t m = 0, n = 0, rk_[PE], rc_[PE], rl_[PE];
+#pragma unroll
+        for (uint32_t u = 0; u < PE; ++u) {
+            const uint32_t e = tid * PE + u;
+            rk_[u] = rc_[u] = rl_[u] = 0;
+            if (e < W && kbin(key[e]) < cut) {
+                m |= 1u << u;
+                ++n;
+                rk_[u] = key[e];
+                rc_[u] = cix[e];
+                rl_[u] = lin[e];
+            }
+        }
+        uint32_t tot;
+        uint32_t o = blk_excl_scan<FNW_F>(n, L.sh, &tot);  // its barriers end every read of lin
+#pragma unroll
+        for (uint32_t u = 0; u < PE; ++u) {
+            const uint32_t e = tid * PE + u;
+            if (m >> u & 1u) {
+                kk[o] = rk_[u];
+                kc[o] = rc_[u];
+                kl[o] = rl_[u];
+                if (tail_in && e == D.Wtot) L.tail_e = o;
+                ++o;
+            }
+        }
+        __syncthreads();
+    }
+    LF_STAMP(4);
+    // order: (key desc, right-first pre-order of the start position asc)
+    auto before = [&](uint32_t kf, uint32_t rf, uint32_t ke, uint32_t re) { return kf > ke || (kf == ke && rf < re); };
+    // ---- the tail's rank (every ranker), then the pops P of tv16fill.hip ----
+    const uint32_t te = L.tail_e;
+    if (te != NONE) {
+        const uint32_t ke = kk[te], re = rf_key(kc[te]);
+        uint32_t n = 0;
+        for (uint32_t f = tid; f < Wk; f += FILL_WG) n += before(kk[f], rf_key(kc[f]), ke, re);
+        uint32_t tot;
+        (void)blk_excl_scan<FNW_F>(n, L.sh, &tot);
+        if (tid == 0) L.tail_rank = tot;
+        __syncthreads();
+    }
+    const uint32_t tr = te != NONE ? L.tail_rank : NONE;
+    if (te != NONE && covered - (16u - d.tl) < rem) {
+        if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+        return;
+    }
+    auto offset = [&](uint32_t i) { return 16u * i - (tr < i ? 16u - d.tl : 0u); };
+    // P = the first rank whose output offset reaches rem
+    uint32_t P = (rem + 15u) / 16u;
+    if (tr < P) P = (rem + (16u - d.tl) + 15u) / 16u;
+    P = min(P, Wk);
+    // conservative bounds for the fast-path conditions: one more pop than P
+    // (the exact orderer counts its pops in (sum desc, index asc) order)
+    const uint32_t Ph = min(P + 1, Wk - 1);
+    // ---- the key at rank Ph: its bin from the bin starts, then the bin's
+    //      kept entries ranked among themselves ----
+    {
+        constexpr uint32_t PER = NBIN / FILL_WG;
+#pragma unroll
+        for (uint32_t u = 0; u < PER; ++u) {
+            const uint32_t b = PER * tid + u;
+            const uint32_t lo = L.bin[b], hi = b + 1 < NBIN ? L.bin[b + 1] : Wk;
+            if (b < cut && lo <= Ph && Ph < hi) L.kh = b;
+        }
+        __syncthreads();
+        const uint32_t bh = L.kh;
+        for (uint32_t f = tid; f < Wk; f += FILL_WG)
+            if (kbin(kk[f]) == bh) {
+                const uint32_t i = atomicAdd(&L.nbl, 1u);
+                if (i < 64) L.bl[i] = kk[f];
+            }
+        __syncthreads();
+        const uint32_t nb = L.nbl;
+        if (nb > 64) {
+            if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+            return;
+        }
+        if (tid < nb) {
+            const uint32_t k = L.bl[tid];
+            uint32_t gt = 0, eq = 0;
+            for (uint32_t i = 0; i < nb; ++i) { gt += L.bl[i] > k; eq += L.bl[i] == k; }
+            const uint32_t at = Ph - L.bin[bh];
+            if (gt <= at && at < gt + eq) L.kh = k;
+        }
+        __syncthreads();
+    }
+    LF_STAMP(5);
+    const uint32_t KH = L.kh;  // R: the kept lines with key >= KH
+    const uint32_t late = D.N > Ph + 1 ? D.N - (Ph + 1) : 0u;  // start positions >= late: the last Ph + 1
+    // ---- this ranker's share: ranks by counting, 64 entries per group, 8
+    //      threads per entry over the kept lines; tie and structure checks ----
+    const uint32_t nr = A.rankers, per = (Wk + nr - 1) / nr;
+    const uint32_t s0 = min(Wk, rk * per), s1 = min(Wk, s0 + per);
+    uint32_t fl = 0;
+    const bool vec = aligned16(d) && (D.cnt & 3u) == 0;
+    for (uint32_t b0 = s0; b0 < s1; b0 += 64) {
+        const uint32_t j = tid & 63u, part = tid >> 6, e = b0 + j;
+        const bool on = e < s1;
+        if (tid < 64) L.rcnt[tid] = 0;
+        __syncthreads();
+        uint32_t rank = 0;
+        if (on) {
+            const uint32_t ke = kk[e], ce = kc[e], re = rf_key(ce), qe = ce + 1;
+            const bool inR = ke >= KH, lt = inR && ce >= late && ce;
+            const uint32_t par = (ce - 1) / 2, sib = ((ce - 1) ^ 1u) + 1;
+            for (uint32_t f = part; f < Wk; f += FNW_F) {
+                const uint32_t kf = kk[f], cf = kc[f];
+                rank += before(kf, rf_key(cf), ke, re);
+                if (f != e && kf == ke && inR) {
+                    fl |= LF_TIES;
+                    if (is_desc(cf + 1, qe)) fl |= LF_VIOL;  // (3): a tied line starting below this one
+                }
+                if (lt && kf >= KH && (cf == par || cf == sib)) fl |= LF_VIOL;  // (3): R at a late line's parent or sibling
+            }
+            atomicAdd(&L.rcnt[j], rank);
+        }
+        __syncthreads();
+        // emit: four lanes per line, the first 256 threads (64 lines)
+        if (tid < 256) {
+            const uint32_t jj = tid >> 2, q = tid & 3u, ee = b0 + jj;
+            if (ee < s1) {
+                const uint32_t i = L.rcnt[jj];
+                const uint32_t off = offset(i);
+                if (i < P && off < rem) {
+                    const uint32_t len = min(i == tr ? d.tl : 16u, rem - off);
+                    const uint32_t pos = kl[ee] * 16, o = D.cnt + off + 4 * q, bi = pos + 4 * q + (uint32_t)d.idx_offset;
+                    if (vec && len == 16 && (off & 3u) == 0) {
+                        *reinterpret_cast<float4 *>(d.val + o) = reinterpret_cast<const float4 *>(d.src + pos)[q];
+                        *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                    } else {
+                        for (uint32_t cc = 0; cc < 4; ++cc)
+                            if (4 * q + cc < len) {
+                                d.val[o + cc] = d.src[(size_t)pos + 4 * q + cc];
+                                d.idx[o + cc] = bi + cc;
+                            }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    LF_STAMP(6);
+    fl = __syncthreads_or((int)(fl & LF_TIES)) ? (fl | LF_TIES) : fl;
+    const bool viol = __syncthreads_or((int)(fl & LF_VIOL));
+    const bool ties = fl & LF_TIES;
+    if (tid == 0 && (viol || ties)) g_or(&A.cc->pad[5], (ties ? LF_TIES : 0u) | (viol ? LF_VIOL : 0u));
+    if (STG_FILL_STAMPS && rk == 0 && tid == 0) { A.dbg[44] = Wk; A.dbg[45] = P; A.dbg[46] = D.Wtot; A.dbg[47] = fl; }
+    LF_STAMP(7);
+    if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[43] = (uint32_t)__builtin_amdgcn_s_memtime();
+}

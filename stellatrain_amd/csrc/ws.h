@@ -79,6 +79,14 @@ struct RSel {
     uint32_t hist[RS_SHARDS][RS_BINS];
 };
 
+// thresholdv16 one-bucket path: a scan launch with no waits between
+// workgroups (tv16_lscan, tv16lone.hip) lists, per chunk, its qualifying and
+// window lines; the fill launch (tv16fill.hip, lfin mode) finishes the call.
+constexpr uint32_t LCHUNK = 512;  // lines (16 floats) per chunk = 32 KiB: one per 256-thread workgroup
+constexpr uint32_t LQCAP = 64;    // qualifying lines listed per chunk (~5 at k = 1 %; more: the finish re-reads it)
+constexpr uint32_t LWCAP = 32;    // window lines listed per chunk (~2; more: likewise)
+constexpr uint32_t LMAXC = 4096;  // chunks of a bucket the one-bucket path takes (128 MiB)
+
 struct DevWS {
     FillCtl *ctl;
     ChunkDesc *desc;     // thresholdv16 chunk descriptors (grown per launch, zeroed)
@@ -93,6 +101,10 @@ struct DevWS {
     uint32_t *tile_aux;  // per-tile secondary counts (threshold-v max, top-k ties)
     uint32_t *stage_pos; // threshold-v staged positions
     float *stage_val;    // threshold-v staged values
+    uint2 *ldesc;        // one-bucket path: per chunk {qualifying lines, window lines}
+    uint32_t *lq;        // ... the chunk's qualifying lines in order (LQCAP per chunk, line within the chunk)
+    uint4 *lw;           // ... its window lines in order: {sum bits, line within the chunk, qualifying before, 0}
+    float4 *lv;          // ... the qualifying lines' data (LQCAP x 4 float4 per chunk)
 };
 
 // ---- launchers (implemented in the .hip files) ----
@@ -120,6 +132,7 @@ struct Tv16Launch {
     uint32_t max_wg;     // fused-kernel workgroups at most (its share of 2 per CU)
     uint32_t desc_cap;   // ChunkDesc entries at ws.desc
     hipEvent_t scan_done;  // optional: recorded between the scan and the fill launch
+    uint32_t lone_cap;   // chunks the one-bucket lists (ws.ldesc / lq / lw) hold (0: none)
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
 // thresholdv16 regime-B heap fill (tv16fill.hip): one workgroup per bucket
@@ -143,9 +156,40 @@ struct Tv16FillArgs {
     uint32_t mode;         // tests (STG_DEBUG_TV16_FILL): 1 = always the shadow heap, 2 = always the literal heap
     bool lone;             // a one-bucket launch: the fill variant that takes the CU's registers
     uint32_t helpers;      // lone: extra workgroups that emit shares of the order (0: none)
-    CallCtl *cc;           // this call's counters: [pad 0] fill tickets, [1] order ready, [2] pops, [3] tail rank
+    CallCtl *cc;           // this call's counters: [pad 0] fill tickets, [1] order ready, [2] pops, [3] tail rank,
+                           // [4] lfin workers done
+    // lfin: the launch also finishes a one-bucket scan (tv16_lscan): `workers`
+    // workgroups emit the qualifying lines, list the window and decide; the
+    // last of them to finish orders the regime-B fill; `helpers` more emit it
+    bool lfin;
+    uint32_t workers;
+    uint32_t nc;           // chunks of the bucket
+    const uint2 *ldesc;
+    const uint32_t *lq;
+    const uint4 *lw;
+    const float4 *lv;
+    uint32_t rankers;      // workgroups that order the regime-B fill in parallel (0: the orderer alone)
+    KeyState *state;
+    const CallParams *cp;  // {t, inc} as the scan read them
+    float *resid;          // fused error feedback: the ragged tail is copied by the finish
 };
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
+// one-bucket scan (tv16lone.hip): every workgroup streams its chunks and lists
+// them; nothing waits on another workgroup
+struct LScanArgs {
+    const float *src;
+    uint32_t nb;           // full lines
+    uint32_t nc;           // chunks
+    const KeyState *state;
+    CallParams *cp;        // receives {t, inc} as read
+    float *resid;          // fused error feedback (or null)
+    uint2 *ldesc;
+    uint32_t *lq;
+    uint4 *lw;
+    float4 *lv;
+    uint32_t *zero_next;   // the next call's counter block (CallCtl), zeroed here
+};
+hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s);
 
 struct TvLaunch {
     const float *src;

@@ -4,7 +4,10 @@ Runs thresholdv16 AIMD sequences whose regime-B calls tie inside the heap
 fill, with STG_DEBUG_TV16_FILL set by the parent (read once per process:
 0 = production, 1 = always the shadow heap, 2 = always the literal heap),
 checks every call's whole stream against the oracle, and prints the fill's
-path counters (debug words 56..59) as one JSON line.
+path counters (debug words 56..59: the orderer's ways) and the one-bucket
+finish's (48..51: rankers without ties, rankers with ties, the orderer after
+a violation, the orderer for a call the rankers could not take) as one JSON
+line.
 """
 from __future__ import annotations
 
@@ -50,7 +53,7 @@ def main():
     comp.check_device()
     w = (C.c_uint32 * 64)()
     check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
-    print(json.dumps({"ok": True, "calls": calls, "paths": list(w)[56:60],
+    print(json.dumps({"ok": True, "calls": calls, "paths": list(w)[56:60], "lfin": list(w)[48:52],
                       "mode": os.environ.get("STG_DEBUG_TV16_FILL")}), flush=True)
 
 

@@ -3,9 +3,12 @@
 tv16fill.hip orders a regime-B bucket's heap pops one of four ways: no two
 popped sums tie (sum order), ties ordered by right-first pre-order of their
 start positions (when its two checks pass), the shadow heap, or the literal
-make_heap / pop_heap in global memory.  STG_DEBUG_TV16_FILL forces the
-heavier ways, so each is checked against the oracle on the same tie-heavy
-AIMD sequences; the fill's path counters show which way ran.
+make_heap / pop_heap in global memory.  A one-bucket call's finish
+(tv16lfin.h) first lets its rankers order the fill in parallel by the same
+right-first rule and falls back to that orderer when they cannot prove it.
+STG_DEBUG_TV16_FILL forces the heavier ways, so each is checked against the
+oracle on the same tie-heavy AIMD sequences; the path counters show which way
+ran.
 """
 from __future__ import annotations
 
@@ -21,8 +24,8 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _child(mode: int):
-    env = dict(os.environ, STG_DEBUG_TV16_FILL=str(mode))
+def _child(mode: int, **extra):
+    env = dict(os.environ, STG_DEBUG_TV16_FILL=str(mode), **extra)
     r = subprocess.run([sys.executable, os.path.join(HERE, "fill_mode_child.py")],
                        capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -30,10 +33,29 @@ def _child(mode: int):
 
 
 def test_production_order(gpu):
+    """Every call here is one bucket: the one-bucket finish's rankers order
+    the regime-B fills (tv16lfin.h); D1's regime-B calls tie among the pops."""
     out = _child(0)
+    plain, tied, viol, notake = out["lfin"]
+    assert tied > 0, out
+    assert out["paths"][3] == 0, out  # never the literal heap
+
+
+def test_production_order_orderer_alone(gpu):
+    """The one-bucket finish without rankers: its last workgroup runs the
+    orderer (tv16fill.hip) on every regime-B call."""
+    out = _child(0, STG_TV16_LFIN_RANKERS="0")
     none, by_start, shadow, literal = out["paths"]
-    assert by_start > 0, out  # D1's regime-B calls tie among the pops
-    assert literal == 0, out
+    assert by_start > 0 and literal == 0, out
+    assert out["lfin"] == [0, 0, 0, 0], out
+
+
+def test_production_order_batched_lone_fill(gpu):
+    """The batched scan for a lone bucket (STG_TV16_LFIN=0): its fill with
+    helper workgroups."""
+    out = _child(0, STG_TV16_LFIN="0")
+    none, by_start, shadow, literal = out["paths"]
+    assert by_start > 0 and literal == 0, out
 
 
 def test_shadow_heap_order(gpu):

@@ -46,6 +46,8 @@ for s in "$@"; do
         ubench) step ubench 300 python tools/ubench_read.py ;;
         configs) step configs 500 python tools/bench_configs.py ;;
         single) step single 200 python tools/bench_configs.py --only single ;;
+        prof_single) step prof_single 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_single" -o run \
+                -- python3 tools/bench_configs.py --only single ;;
         c2) step c2 300 python tools/bench_configs.py --only c2 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
@@ -74,6 +76,8 @@ for s in "$@"; do
                 step streams_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
                 STG_TV16_SERIAL=1 step streams_serial_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
             done ;;
+        lfin_probe) step lfin_probe 200 python tools/lfin_probe.py ;;
+        lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step lfin_stamps 200 python tools/lfin_probe.py ;;
         fill_stamps) FS_BUCKETS=16 FS_PARITY=1 STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so \
                 step fill_stamps 200 python tools/fill_stamps.py ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
