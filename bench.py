@@ -222,9 +222,6 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend == "oracle":
         return main_oracle(args, world, rank)
-    if args.streams > 1:
-        # S concurrent persistent launches sharing the device's workgroup slots
-        os.environ.setdefault("STG_TV16_INFLIGHT", str(args.streams))
     import torch
     import torch.distributed as dist
     if world > 1:

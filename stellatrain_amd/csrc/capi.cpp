@@ -162,7 +162,7 @@ struct Workspace {
         cap_lone = 0;
         HIP_TRY(hipMalloc(&d.ldesc, c * sizeof(uint2)));
         HIP_TRY(hipMalloc(&d.lq, c * stg::LQCAP * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&d.lw, c * stg::LWCAP * sizeof(uint4)));
+        HIP_TRY(hipMalloc(&d.lw, c * stg::LWCAP * sizeof(uint2)));
         HIP_TRY(hipMalloc(&d.lv, c * stg::LQCAP * 4 * sizeof(float4)));
         cap_lone = c;
         return STG_OK;
@@ -316,9 +316,12 @@ std::string state_key(Method m, const char *key, const void *src) {
 //    event hand-off between streams costs more than it hides, and launches
 //    from three or four streams overlap each other's tails and fills anyway
 //    (profiles/r02_streams.jsonl).
-//  * STG_TV16_INFLIGHT (1-4, default 1) launches per device in flight: a
-//    launch on stream s first makes s wait for the oldest in-flight launch of
-//    another stream when the lane is full.
+//  * STG_TV16_INFLIGHT (1-4; default unlimited) launches per device in
+//    flight: a launch on stream s first makes s wait for the oldest in-flight
+//    launch of another stream when the lane is full.  Unlimited (the default)
+//    records no events at all: concurrent callers on their own streams
+//    overlap freely (the reference's per-task compress() from many pool
+//    workers, engine/modules/compress.cpp:141, core_module_api.cpp:7-24).
 struct FusedLane {
     std::mutex mu;
     std::vector<std::pair<hipEvent_t, hipStream_t>> inflight;  // oldest first
@@ -333,13 +336,13 @@ bool tv16_serial() {
 }
 FusedLane g_lanes[64];
 
-uint32_t fused_inflight() {
+uint32_t fused_inflight() {  // 0: unlimited
     static const uint32_t v = [] {
         if (const char *e = getenv("STG_TV16_INFLIGHT")) {
             const int x = atoi(e);
-            return (uint32_t)std::min(4, std::max(1, x));
+            return x <= 0 ? 0u : (uint32_t)std::min(4, x);
         }
-        return 1u;
+        return 0u;
     }();
     return v;
 }
@@ -412,13 +415,18 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     // simply interleave as slots free up (STG_TV16_SHARE=1 splits the slots
     // evenly between the in-flight launches instead).
     static const bool share = getenv("STG_TV16_SHARE") && atoi(getenv("STG_TV16_SHARE")) == 1;
-    a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / inflight * XCDS)
+    a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / std::max(inflight, 4u) * XCDS)
                      : (uint32_t)(2 * h->num_cu);
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     a.lone_cap = (uint32_t)ws->cap_lone;
+    if (!inflight && !tv16_serial()) {  // no admission: nothing to track
+        HIP_TRY(stg::launch_tv16(a, ws->d, s));
+        grp.clear();
+        return STG_OK;
+    }
     FusedLane &lane = g_lanes[h->device & 63];
     std::lock_guard<std::mutex> lg(lane.mu);
-    const size_t max_inflight = inflight;
+    const size_t max_inflight = inflight ? inflight : 64;
     while (lane.inflight.size() >= max_inflight) {
         auto old = lane.inflight.front();
         lane.inflight.erase(lane.inflight.begin());

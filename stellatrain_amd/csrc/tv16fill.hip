@@ -382,9 +382,6 @@ __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uin
 
 #include "tv16lfin.h"
 
-#ifndef STG_FILL_STAMPS
-#define STG_FILL_STAMPS 0
-#endif
 // Registers for 8 waves per SIMD (<= 64 VGPRs): the workgroup's two waves per
 // SIMD run beside the six of two scan workgroups.  The LDS is dynamic: the
 // compiler derives the occupancy it aims for from static LDS and would widen
@@ -442,6 +439,11 @@ tv16_fill(Tv16FillArgs A) {
         __syncthreads();
         if (tid == 0) s_last = g_add(&A.cc->pad[4], 1u) == A.workers + A.rankers - 1;
         __syncthreads();
+        if (STG_FILL_STAMPS && tid == 0) {  // diagnostics: each role's arrival (words 24..27: worker 0, ranker 0, last)
+            if (role == 0) A.dbg[24] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            if (role == A.workers) A.dbg[25] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            if (s_last) { A.dbg[26] = (uint32_t)__builtin_amdgcn_s_memrealtime(); A.dbg[27] = role; }
+        }
         if (!s_last) return;
         const uint32_t rep = ld_sc1(&A.cc->pad[5]);
         // how the call's fill was ordered (debug words 48..51: rankers without

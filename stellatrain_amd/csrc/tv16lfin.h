@@ -7,7 +7,8 @@
 // ragged tail, AIMD) and the regime-B heap fill (:261-293).
 //
 // The scan left per chunk of LCHUNK lines its counts (ldesc), its qualifying
-// lines in order with their data (lq, lv) and its window lines in order (lw).
+// lines in order with their data (lq, lv) and its window lines in order (lw:
+// {sum bits, line within the chunk | qualifying lines before it << 16}).
 // Three roles share the launch, none waits on another:
 //   workers  (tickets [0, workers))  take the chunks' prefix counts, decide
 //            the regime exactly as the batched scan's last chunk does
@@ -35,7 +36,7 @@ struct LfinArgs {
     uint32_t nc, workers, rankers, epoch, mode;
     const uint2 *ldesc;
     const uint32_t *lq;
-    const uint4 *lw;
+    const uint2 *lw;
     const float4 *lv;
     KeyState *state;
     const CallParams *cp;
@@ -50,25 +51,27 @@ struct LfinLds {
     uint32_t qp[LMAXC + 1];  // per chunk: exclusive prefix of qualifying lines (+ total)
     uint32_t wp[LMAXC + 1];  // ... of window lines
     union {
-        struct {               // ranker: the window, by entry (scan order)
-            uint32_t key[CAND_CAP + 1];  // order key ford(line sum); the ragged tail last
-            uint32_t cix[CAND_CAP + 1];  // candidate index = the line's start heap position
-            uint32_t lin[CAND_CAP + 1];  // line (the tail: nb); first the entry's chunk
+        struct {                       // ranker
+            uint16_t emap[CAND_CAP];   // window entry -> its chunk
+            uint32_t kk[EMAX];         // kept lines: order key ford(line sum)
+            uint32_t kc[EMAX];         // ... candidate index (start heap position)
+            uint32_t kr[EMAX];         // ... right-first pre-order key of the start position
+            uint32_t kl[EMAX];         // ... line (the ragged tail: nb)
+            uint16_t bl2[EMAX];        // kept lines grouped by bin
+            uint16_t rr[EMAX];         // this ranker's share: rank of each
+            uint32_t cur[NBIN];        // bin cursors
         } r;
-        struct {               // worker: rank -> chunk
+        struct {                       // worker: rank -> chunk
             uint16_t qmap[LF_QMAP];
         } w;
     } u;
     uint32_t bin[NBIN];        // ranker: window histogram -> bin starts
     uint32_t sh[32];
-    uint32_t bl[64];           // the bin holding rank pc: its kept entries
-    uint32_t rcnt[64];         // rank partial counts of the current group of 64 entries
-    uint32_t cut, wk, nbl, tail_e, tail_rank, kh, flags;
+    uint32_t bl[64];           // the bin holding rank Ph: its kept keys
+    uint32_t late[64];         // this ranker's lines of R starting in the last Ph + 1 positions
+    uint32_t cut, wk, nbl, tail_e, tail_rank, kh, nlate;
     LfinArgs args;
 };
-// the kept lines, compacted: keys and candidate indices over qp / wp (no
-// longer read by then), lines in place over the window's lines
-static_assert(2 * EMAX * sizeof(uint32_t) <= 2 * (LMAXC + 1) * sizeof(uint32_t), "kept lines fit over the prefixes");
 
 __device__ __forceinline__ uint32_t chunk_of(const uint32_t *p, uint32_t nc, uint32_t g) {
     uint32_t lo = 0, hi = nc;  // the last c < nc with p[c] <= g (p ascending, p[0] = 0)
@@ -88,10 +91,19 @@ constexpr uint32_t LF_RANKED = 8u;    // a regime-B call the rankers took
 #ifndef STG_FILL_STAMPS
 #define STG_FILL_STAMPS 0
 #endif
-// diagnostics (STG_FILL_STAMPS builds): ranker 0's phase stamps, words 32..47
+// diagnostics (STG_FILL_STAMPS builds): ranker 0's phase stamps, words 32..47;
+// worker 0's, words 16..23
+#define LF_WSTAMP(i)                                                                                 \
+    do {                                                                                             \
+        if (STG_FILL_STAMPS && wk == 0 && threadIdx.x == 0)                                          \
+            A.dbg[16 + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime();                            \
+    } while (0)
+#ifndef STG_FILL_STAMPS_RK
+#define STG_FILL_STAMPS_RK 0  // the ranker whose phases are stamped
+#endif
 #define LF_STAMP(i)                                                                                  \
     do {                                                                                             \
-        if (STG_FILL_STAMPS && rk == 0 && threadIdx.x == 0)                                          \
+        if (STG_FILL_STAMPS && rk == STG_FILL_STAMPS_RK && threadIdx.x == 0)                         \
             A.dbg[32 + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime();                            \
     } while (0)
 
@@ -206,7 +218,9 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
     const Tv16FillBucket &d = A.d;
     const uint32_t tid = threadIdx.x, nc = A.nc, nwk = A.workers;
     LfinDec D;
+    LF_WSTAMP(0);
     lfin_prefix(L, A, D);
+    LF_WSTAMP(1);
     const uint32_t *qp = L.qp, *wp = L.wp;
     const bool vec = aligned16(d);
     // ---- this worker's share of the qualifying lines, by global rank; a map
@@ -260,6 +274,7 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
         }
         __syncthreads();
     }
+    LF_WSTAMP(2);
     // ---- regime B: this worker's share of the window list, in scan order
     //      (the exact orderer's input), one thread per (chunk, slot) ----
     uint32_t *cu = const_cast<uint32_t *>(d.cand), *cl = cu + CAND_CAP, *ci = cu + 2 * CAND_CAP;
@@ -269,13 +284,14 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
             const uint32_t c = c_lo + p / LWCAP, i = p % LWCAP;
             const uint32_t wc = wp[c + 1] - wp[c];
             if (i >= wc || wc > LWCAP || qp[c + 1] - qp[c] > LQCAP) continue;  // overflowed: re-read below
-            const uint4 x = A.lw[(size_t)c * LWCAP + i];
-            const uint32_t line = c * LCHUNK + x.y, e = wp[c] + i;
+            const uint2 x = A.lw[(size_t)c * LWCAP + i];
+            const uint32_t line = c * LCHUNK + (x.y & 0xffffu), e = wp[c] + i;
             st_sc1(&cu[e], x.x);
             st_sc1(&cl[e], line * 16);
-            st_sc1(&ci[e], line - (qp[c] + x.z));
+            st_sc1(&ci[e], line - (qp[c] + (x.y >> 16)));
         }
     }
+    LF_WSTAMP(3);
     // ---- this worker's chunks whose lists overflowed: read again ----
     if (!D.lists_ok) {
         for (uint32_t c = c_lo; c < c_hi; ++c) {
@@ -285,6 +301,7 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
             if (emit || list) lfin_rescan(L, d, c, D, emit, list);
         }
     }
+    LF_WSTAMP(4);
     // ---- worker 0: tail, AIMD state, count, decision (tv16.hip finish_chunk) ----
     if (wk == 0 && tid == 0) {
         if (D.ct) {
@@ -310,6 +327,7 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
         vm_drain();
         st_sc1(&Dc.w[0], ((uint64_t)((A.epoch << 8) | TV16_TAG_DEC) << 32) | flags);
     }
+    LF_WSTAMP(5);
 }
 
 // ---------------------------------------------------------------------------
@@ -338,228 +356,215 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
         return;
     }
-    // ---- the window in LDS: entry -> chunk (one thread per chunk), then
-    //      every entry's load in flight together ----
-    uint32_t *const key = L.u.r.key, *const cix = L.u.r.cix, *const lin = L.u.r.lin;
-    for (uint32_t c = tid; c < nc; c += FILL_WG)
-        for (uint32_t e = L.wp[c]; e < L.wp[c + 1]; ++e) lin[e] = c;
-    __syncthreads();
-    constexpr uint32_t KW = 8;
-    for (uint32_t e0 = tid; e0 < D.Wtot; e0 += KW * FILL_WG) {
-        uint4 x[KW];
-        uint32_t c[KW];
-#pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) {
-            const uint32_t e = e0 + k * FILL_WG;
-            if (e < D.Wtot) {
-                c[k] = lin[e];
-                x[k] = A.lw[(size_t)c[k] * LWCAP + (e - L.wp[c[k]])];
-            }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) {
-            const uint32_t e = e0 + k * FILL_WG;
-            if (e < D.Wtot) {
-                const uint32_t line = c[k] * LCHUNK + x[k].y;
-                key[e] = ford(u2f(x[k].x));
-                cix[e] = line - (L.qp[c[k]] + x[k].z);
-                lin[e] = line;
-            }
-        }
-    }
-    LF_STAMP(2);
-    if (tail_in && tid == 0) {  // the ragged tail: the candidate vector's last entry (thresholdv16.cpp:229-234)
-        key[D.Wtot] = ford(D.tail_key);
-        cix[D.Wtot] = D.N - 1;
-        lin[D.Wtot] = d.nb;
-    }
-    // ---- histogram of 256-ulp bins below t (sum descending); keep the first
-    //      bins holding M + 2 entries: every pop, the first line past them and
-    //      its ties (a bin never splits equal sums) ----
-    for (uint32_t i = tid; i < NBIN; i += FILL_WG) L.bin[i] = 0;
-    __syncthreads();
-    auto kbin = [&](uint32_t ok) -> uint32_t {  // ok = ford(sum)
+    auto kbin = [&](uint32_t ok) -> uint32_t {  // 256-ulp bins below t, sum descending (ok = ford(sum))
         const float k = u2f(ok & 0x80000000u ? ok & 0x7fffffffu : ~ok);
         if (k >= D.t) return 0u;
         if (!(k > 0.f)) return NBIN - 1;
         return min((tb - 1u - f2u(k)) >> 8, NBIN - 1);
     };
-    for (uint32_t e = tid; e < W; e += FILL_WG) atomicAdd(&L.bin[kbin(key[e])], 1u);
+    // ---- the window: entry -> chunk (a thread per chunk), then each
+    //      thread's entries loaded together into registers, binned there ----
+    for (uint32_t c = tid; c < nc; c += FILL_WG)
+        for (uint32_t e = L.wp[c]; e < L.wp[c + 1]; ++e) L.u.r.emap[e] = (uint16_t)c;
+    for (uint32_t i = tid; i < NBIN; i += FILL_WG) L.bin[i] = 0;
     __syncthreads();
+    constexpr uint32_t KW = CAND_CAP / FILL_WG;  // entries per thread: e = tid + k * FILL_WG
+    static_assert(KW * FILL_WG == CAND_CAP, "window entries per thread");
+    uint32_t ok[KW], cx[KW], ln[KW];
+    {
+        uint2 x[KW];
+        uint32_t c[KW];
+#pragma unroll
+        for (uint32_t k = 0; k < KW; ++k) {
+            const uint32_t e = tid + k * FILL_WG;
+            c[k] = 0;
+            if (e < D.Wtot) {
+                c[k] = L.u.r.emap[e];
+                x[k] = A.lw[(size_t)c[k] * LWCAP + (e - L.wp[c[k]])];
+            }
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < KW; ++k) {
+            const uint32_t e = tid + k * FILL_WG;
+            ok[k] = 0;
+            if (e < D.Wtot) {
+                const uint32_t line = c[k] * LCHUNK + (x[k].y & 0xffffu);
+                ok[k] = ford(u2f(x[k].x));
+                cx[k] = line - (L.qp[c[k]] + (x[k].y >> 16));
+                ln[k] = line;
+            } else if (e == D.Wtot && tail_in) {  // the ragged tail: the candidate vector's last entry
+                ok[k] = ford(D.tail_key);          // (thresholdv16.cpp:229-234)
+                cx[k] = D.N - 1;
+                ln[k] = d.nb;
+            }
+            if (e < W) atomicAdd(&L.bin[kbin(ok[k])], 1u);
+        }
+    }
+    __syncthreads();
+    LF_STAMP(2);
+    // ---- keep the first bins holding M + 2 entries: every pop, the first
+    //      line past them and its ties (a bin never splits equal sums) ----
     {
         constexpr uint32_t PER = NBIN / FILL_WG;
         static_assert(PER == 2, "two bins per thread");
         const uint32_t b0 = L.bin[PER * tid], b1 = L.bin[PER * tid + 1], need = D.M + 2;
         uint32_t tot;
         const uint32_t run = blk_excl_scan<FNW_F>(b0 + b1, L.sh, &tot);
-        L.bin[PER * tid] = run;
-        L.bin[PER * tid + 1] = run + b0;
+        L.bin[PER * tid] = L.u.r.cur[PER * tid] = run;
+        L.bin[PER * tid + 1] = L.u.r.cur[PER * tid + 1] = run + b0;
         if (run < need && run + b0 >= need) { L.cut = PER * tid + 1; L.wk = run + b0; }
         else if (run + b0 < need && run + b0 + b1 >= need) { L.cut = PER * tid + 2; L.wk = run + b0 + b1; }
         if (tid == 0 && tot < need) { L.cut = NBIN; L.wk = tot; }
-        if (tid == 0) { L.tail_e = NONE; L.nbl = 0; L.flags = 0; }
+        if (tid == 0) { L.tail_e = NONE; L.nbl = 0; L.nlate = 0; }
         __syncthreads();
     }
-    LF_STAMP(3);
     const uint32_t cut = L.cut, Wk = L.wk;
     const uint32_t rem = d.dst_len - D.cnt;
-    const uint32_t covered = 16u * Wk;  // less 16 - tl if the tail is kept (checked below)
-    if (Wk > EMAX || Wk == 0 || covered < rem) {
+    if (Wk > EMAX || Wk == 0 || 16u * Wk < rem) {
         if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
         return;
     }
-    // ---- the kept lines, compacted (over qp / wp) in entry order ----
-    uint32_t *const kk = L.qp, *const kc = L.qp + EMAX, *const kl = lin;
+    LF_STAMP(3);
+    // ---- the kept lines, compacted from registers, and grouped by bin ----
+    uint32_t *const kk = L.u.r.kk, *const kc = L.u.r.kc, *const kr = L.u.r.kr, *const kl = L.u.r.kl;
     {
-        constexpr uint32_t PE = CAND_CAP / FILL_WG + 1;
-        uint32_t m = 0, n = 0, rk_[PE], rc_[PE], rl_[PE];
+        uint32_t n = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < PE; ++u) {
-            const uint32_t e = tid * PE + u;
-            rk_[u] = rc_[u] = rl_[u] = 0;
-            if (e < W && kbin(key[e]) < cut) {
-                m |= 1u << u;
-                ++n;
-                rk_[u] = key[e];
-                rc_[u] = cix[e];
-                rl_[u] = lin[e];
-            }
-        }
+        for (uint32_t k = 0; k < KW; ++k) n += (tid + k * FILL_WG < W && kbin(ok[k]) < cut) ? 1u : 0u;
         uint32_t tot;
-        uint32_t o = blk_excl_scan<FNW_F>(n, L.sh, &tot);  // its barriers end every read of lin
+        uint32_t o = blk_excl_scan<FNW_F>(n, L.sh, &tot);
 #pragma unroll
-        for (uint32_t u = 0; u < PE; ++u) {
-            const uint32_t e = tid * PE + u;
-            if (m >> u & 1u) {
-                kk[o] = rk_[u];
-                kc[o] = rc_[u];
-                kl[o] = rl_[u];
-                if (tail_in && e == D.Wtot) L.tail_e = o;
-                ++o;
+        for (uint32_t k = 0; k < KW; ++k) {
+            const uint32_t e = tid + k * FILL_WG;
+            if (e < W) {
+                const uint32_t b = kbin(ok[k]);
+                if (b < cut) {
+                    kk[o] = ok[k];
+                    kc[o] = cx[k];
+                    kr[o] = rf_key(cx[k]);
+                    kl[o] = ln[k];
+                    L.u.r.bl2[atomicAdd(&L.u.r.cur[b], 1u)] = (uint16_t)o;
+                    if (e == D.Wtot) L.tail_e = o;
+                    ++o;
+                }
             }
         }
         __syncthreads();
     }
     LF_STAMP(4);
     // order: (key desc, right-first pre-order of the start position asc)
-    auto before = [&](uint32_t kf, uint32_t rf, uint32_t ke, uint32_t re) { return kf > ke || (kf == ke && rf < re); };
-    // ---- the tail's rank (every ranker), then the pops P of tv16fill.hip ----
+    auto before = [&](uint32_t f, uint32_t e) { return kk[f] > kk[e] || (kk[f] == kk[e] && kr[f] < kr[e]); };
+    auto rank_of = [&](uint32_t e) {  // its bin's start + the bin's lines before it
+        const uint32_t b = kbin(kk[e]), hi = L.u.r.cur[b];
+        uint32_t r = L.bin[b];
+        for (uint32_t x = L.bin[b]; x < hi; ++x) r += before(L.u.r.bl2[x], e);
+        return r;
+    };
+    // ---- the tail's rank, then the pops P of tv16fill.hip ----
     const uint32_t te = L.tail_e;
-    if (te != NONE) {
-        const uint32_t ke = kk[te], re = rf_key(kc[te]);
-        uint32_t n = 0;
-        for (uint32_t f = tid; f < Wk; f += FILL_WG) n += before(kk[f], rf_key(kc[f]), ke, re);
-        uint32_t tot;
-        (void)blk_excl_scan<FNW_F>(n, L.sh, &tot);
-        if (tid == 0) L.tail_rank = tot;
-        __syncthreads();
-    }
+    if (te != NONE && tid == 0) L.tail_rank = rank_of(te);
+    __syncthreads();
     const uint32_t tr = te != NONE ? L.tail_rank : NONE;
-    if (te != NONE && covered - (16u - d.tl) < rem) {
+    if (te != NONE && 16u * Wk - (16u - d.tl) < rem) {
         if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
         return;
     }
-    auto offset = [&](uint32_t i) { return 16u * i - (tr < i ? 16u - d.tl : 0u); };
-    // P = the first rank whose output offset reaches rem
-    uint32_t P = (rem + 15u) / 16u;
+    uint32_t P = (rem + 15u) / 16u;  // the first rank whose output offset reaches rem
     if (tr < P) P = (rem + (16u - d.tl) + 15u) / 16u;
     P = min(P, Wk);
     // conservative bounds for the fast-path conditions: one more pop than P
     // (the exact orderer counts its pops in (sum desc, index asc) order)
     const uint32_t Ph = min(P + 1, Wk - 1);
-    // ---- the key at rank Ph: its bin from the bin starts, then the bin's
-    //      kept entries ranked among themselves ----
+    // ---- the key at rank Ph: its bin, then the bin's keys ranked among themselves ----
     {
         constexpr uint32_t PER = NBIN / FILL_WG;
 #pragma unroll
         for (uint32_t u = 0; u < PER; ++u) {
             const uint32_t b = PER * tid + u;
-            const uint32_t lo = L.bin[b], hi = b + 1 < NBIN ? L.bin[b + 1] : Wk;
-            if (b < cut && lo <= Ph && Ph < hi) L.kh = b;
+            if (b < cut && L.bin[b] <= Ph && Ph < L.u.r.cur[b]) L.kh = b;
         }
         __syncthreads();
-        const uint32_t bh = L.kh;
-        for (uint32_t f = tid; f < Wk; f += FILL_WG)
-            if (kbin(kk[f]) == bh) {
-                const uint32_t i = atomicAdd(&L.nbl, 1u);
-                if (i < 64) L.bl[i] = kk[f];
-            }
-        __syncthreads();
-        const uint32_t nb = L.nbl;
+        const uint32_t bh = L.kh, lo = L.bin[bh], nb = L.u.r.cur[bh] - lo;
         if (nb > 64) {
             if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
             return;
         }
+        if (tid < nb) L.bl[tid] = kk[L.u.r.bl2[lo + tid]];
+        __syncthreads();
         if (tid < nb) {
             const uint32_t k = L.bl[tid];
             uint32_t gt = 0, eq = 0;
             for (uint32_t i = 0; i < nb; ++i) { gt += L.bl[i] > k; eq += L.bl[i] == k; }
-            const uint32_t at = Ph - L.bin[bh];
-            if (gt <= at && at < gt + eq) L.kh = k;
+            if (gt <= Ph - lo && Ph - lo < gt + eq) L.kh = k;
         }
         __syncthreads();
     }
     LF_STAMP(5);
     const uint32_t KH = L.kh;  // R: the kept lines with key >= KH
     const uint32_t late = D.N > Ph + 1 ? D.N - (Ph + 1) : 0u;  // start positions >= late: the last Ph + 1
-    // ---- this ranker's share: ranks by counting, 64 entries per group, 8
-    //      threads per entry over the kept lines; tie and structure checks ----
+    // ---- this ranker's share: a thread per line, its rank within its bin;
+    //      tie and structure checks (tv16fill.hip (3)) ----
     const uint32_t nr = A.rankers, per = (Wk + nr - 1) / nr;
     const uint32_t s0 = min(Wk, rk * per), s1 = min(Wk, s0 + per);
     uint32_t fl = 0;
-    const bool vec = aligned16(d) && (D.cnt & 3u) == 0;
-    for (uint32_t b0 = s0; b0 < s1; b0 += 64) {
-        const uint32_t j = tid & 63u, part = tid >> 6, e = b0 + j;
-        const bool on = e < s1;
-        if (tid < 64) L.rcnt[tid] = 0;
-        __syncthreads();
-        uint32_t rank = 0;
-        if (on) {
-            const uint32_t ke = kk[e], ce = kc[e], re = rf_key(ce), qe = ce + 1;
-            const bool inR = ke >= KH, lt = inR && ce >= late && ce;
-            const uint32_t par = (ce - 1) / 2, sib = ((ce - 1) ^ 1u) + 1;
-            for (uint32_t f = part; f < Wk; f += FNW_F) {
-                const uint32_t kf = kk[f], cf = kc[f];
-                rank += before(kf, rf_key(cf), ke, re);
-                if (f != e && kf == ke && inR) {
-                    fl |= LF_TIES;
-                    if (is_desc(cf + 1, qe)) fl |= LF_VIOL;  // (3): a tied line starting below this one
-                }
-                if (lt && kf >= KH && (cf == par || cf == sib)) fl |= LF_VIOL;  // (3): R at a late line's parent or sibling
-            }
-            atomicAdd(&L.rcnt[j], rank);
-        }
-        __syncthreads();
-        // emit: four lanes per line, the first 256 threads (64 lines)
-        if (tid < 256) {
-            const uint32_t jj = tid >> 2, q = tid & 3u, ee = b0 + jj;
-            if (ee < s1) {
-                const uint32_t i = L.rcnt[jj];
-                const uint32_t off = offset(i);
-                if (i < P && off < rem) {
-                    const uint32_t len = min(i == tr ? d.tl : 16u, rem - off);
-                    const uint32_t pos = kl[ee] * 16, o = D.cnt + off + 4 * q, bi = pos + 4 * q + (uint32_t)d.idx_offset;
-                    if (vec && len == 16 && (off & 3u) == 0) {
-                        *reinterpret_cast<float4 *>(d.val + o) = reinterpret_cast<const float4 *>(d.src + pos)[q];
-                        *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
-                    } else {
-                        for (uint32_t cc = 0; cc < 4; ++cc)
-                            if (4 * q + cc < len) {
-                                d.val[o + cc] = d.src[(size_t)pos + 4 * q + cc];
-                                d.idx[o + cc] = bi + cc;
-                            }
-                    }
-                }
+    for (uint32_t e = s0 + tid; e < s1; e += FILL_WG) {
+        const uint32_t ke = kk[e], ce = kc[e], qe = ce + 1;
+        const bool inR = ke >= KH;
+        const uint32_t b = kbin(ke), hi = L.u.r.cur[b];
+        uint32_t r = L.bin[b];
+        for (uint32_t x = L.bin[b]; x < hi; ++x) {
+            const uint32_t g = L.u.r.bl2[x];
+            r += before(g, e);
+            if (g != e && kk[g] == ke && inR) {
+                fl |= LF_TIES;
+                if (is_desc(kc[g] + 1, qe)) fl |= LF_VIOL;  // (3): a tied line starting below this one
             }
         }
-        __syncthreads();
+        L.u.r.rr[e - s0] = (uint16_t)r;
+        if (inR && ce >= late && ce) {  // a late line of R: checked below by the whole workgroup
+            const uint32_t i = atomicAdd(&L.nlate, 1u);
+            if (i < 64) L.late[i] = ce;
+        }
+    }
+    __syncthreads();
+    {   // (3): no line of R at a late line's parent or sibling -- every thread
+        // takes its kept lines against every late one
+        const uint32_t nl = L.nlate;
+        if (nl > 64) fl |= LF_VIOL;
+        else if (nl)
+            for (uint32_t f = tid; f < Wk; f += FILL_WG) {
+                if (kk[f] < KH) continue;
+                const uint32_t cf = kc[f];
+                for (uint32_t j = 0; j < nl; ++j) {
+                    const uint32_t ce = L.late[j];
+                    if (cf == (ce - 1) / 2 || cf == ((ce - 1) ^ 1u) + 1) fl |= LF_VIOL;
+                }
+            }
     }
     LF_STAMP(6);
-    fl = __syncthreads_or((int)(fl & LF_TIES)) ? (fl | LF_TIES) : fl;
+    // ---- emit the share's pops: four lanes per line ----
+    const bool vec = aligned16(d) && (D.cnt & 3u) == 0;
+    auto offset = [&](uint32_t i) { return 16u * i - (tr < i ? 16u - d.tl : 0u); };
+    for (uint32_t j = s0 + (tid >> 2); j < s1; j += FILL_WG / 4) {
+        const uint32_t q = tid & 3u, i = L.u.r.rr[j - s0], off = offset(i);
+        if (i >= P || off >= rem) continue;
+        const uint32_t len = min(i == tr ? d.tl : 16u, rem - off);
+        const uint32_t pos = kl[j] * 16, o = D.cnt + off + 4 * q, bi = pos + 4 * q + (uint32_t)d.idx_offset;
+        if (vec && len == 16 && (off & 3u) == 0) {
+            *reinterpret_cast<float4 *>(d.val + o) = reinterpret_cast<const float4 *>(d.src + pos)[q];
+            *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+        } else {
+            for (uint32_t cc = 0; cc < 4; ++cc)
+                if (4 * q + cc < len) {
+                    d.val[o + cc] = d.src[(size_t)pos + 4 * q + cc];
+                    d.idx[o + cc] = bi + cc;
+                }
+        }
+    }
+    const bool ties = __syncthreads_or((int)(fl & LF_TIES));
     const bool viol = __syncthreads_or((int)(fl & LF_VIOL));
-    const bool ties = fl & LF_TIES;
     if (tid == 0 && (viol || ties)) g_or(&A.cc->pad[5], (ties ? LF_TIES : 0u) | (viol ? LF_VIOL : 0u));
-    if (STG_FILL_STAMPS && rk == 0 && tid == 0) { A.dbg[44] = Wk; A.dbg[45] = P; A.dbg[46] = D.Wtot; A.dbg[47] = fl; }
+    if (STG_FILL_STAMPS && rk == STG_FILL_STAMPS_RK && tid == 0) { A.dbg[44] = Wk; A.dbg[45] = P; A.dbg[46] = s1 - s0; A.dbg[47] = fl; }
     LF_STAMP(7);
     if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[43] = (uint32_t)__builtin_amdgcn_s_memtime();
 }

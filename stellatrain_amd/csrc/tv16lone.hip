@@ -16,7 +16,7 @@
 //   ldesc[c] = {qualifying lines, window lines}       (true counts)
 //   lq[c][r] = the r-th qualifying line of the chunk   (line within the chunk)
 //   lv[c][r] = its 16 floats (staged from the stream: the finish never re-reads them)
-//   lw[c][r] = {sum bits, line, qualifying lines before it, 0} of its r-th
+//   lw[c][r] = {sum bits, line | qualifying lines before it << 16} of its r-th
 //              window line (sum in [t - 2^18 ulps, t), thresholdv16 regime B)
 // -- and the fill launch that follows (tv16fill.hip, lfin mode) takes the
 // prefixes, decides the regime, emits the qualifying lines in index order and
@@ -58,7 +58,7 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
     const uint32_t qn = uni(lds_ld(&L.qn[sl])), wn = uni(lds_ld(&L.wn[sl]));
     const uint32_t ql = std::min(qn, LQCAP), wlc = std::min(wn, LWCAP);
     uint32_t *lq = A.lq + (size_t)c * LQCAP;
-    uint4 *lw = A.lw + (size_t)c * LWCAP;
+    uint2 *lw = A.lw + (size_t)c * LWCAP;
     float4 *lv = A.lv + (size_t)c * LQCAP * 4;
     // entry e of the list has rank r_e; its line data (four float4) goes to
     // lv[r_e]: lane = 16 entries x 4 quarters per round
@@ -79,7 +79,7 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
         uint32_t r = 0, qb = 0;
         for (uint32_t x = 0; x < wlc; ++x) r += (uint32_t)L.wl[sl][x] < li;
         for (uint32_t x = 0; x < ql; ++x) qb += L.ql[sl][x] < li;
-        if (lane < wlc) lw[r] = make_uint4((uint32_t)(e >> 32), li, qb, 0u);
+        if (lane < wlc) lw[r] = make_uint2((uint32_t)(e >> 32), li | qb << 16);
     }
     if (lane == 0) A.ldesc[c] = make_uint2(qn, wn);
     lds_drain();

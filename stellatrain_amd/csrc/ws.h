@@ -103,7 +103,7 @@ struct DevWS {
     float *stage_val;    // threshold-v staged values
     uint2 *ldesc;        // one-bucket path: per chunk {qualifying lines, window lines}
     uint32_t *lq;        // ... the chunk's qualifying lines in order (LQCAP per chunk, line within the chunk)
-    uint4 *lw;           // ... its window lines in order: {sum bits, line within the chunk, qualifying before, 0}
+    uint2 *lw;           // ... its window lines in order: {sum bits, line within the chunk | qualifying before << 16}
     float4 *lv;          // ... the qualifying lines' data (LQCAP x 4 float4 per chunk)
 };
 
@@ -166,7 +166,7 @@ struct Tv16FillArgs {
     uint32_t nc;           // chunks of the bucket
     const uint2 *ldesc;
     const uint32_t *lq;
-    const uint4 *lw;
+    const uint2 *lw;
     const float4 *lv;
     uint32_t rankers;      // workgroups that order the regime-B fill in parallel (0: the orderer alone)
     KeyState *state;
@@ -185,7 +185,7 @@ struct LScanArgs {
     float *resid;          // fused error feedback (or null)
     uint2 *ldesc;
     uint32_t *lq;
-    uint4 *lw;
+    uint2 *lw;
     float4 *lv;
     uint32_t *zero_next;   // the next call's counter block (CallCtl), zeroed here
 };

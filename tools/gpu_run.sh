@@ -76,7 +76,10 @@ for s in "$@"; do
                 step streams_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
                 STG_TV16_SERIAL=1 step streams_serial_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
             done ;;
+        lone_bench) step lone_bench 200 ./tools/lone_bench 16 96 ;;
+        prof_lone_bench) step prof_lone_bench 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lone_bench" -o run -- ./tools/lone_bench 16 96 ;;
         lfin_probe) step lfin_probe 200 python tools/lfin_probe.py ;;
+        prof_lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step prof_lfin_stamps 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lfin_stamps" -o run -- python3 tools/lfin_probe.py ;;
         lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step lfin_stamps 200 python tools/lfin_probe.py ;;
         fill_stamps) FS_BUCKETS=16 FS_PARITY=1 STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so \
                 step fill_stamps 200 python tools/fill_stamps.py ;;

@@ -48,8 +48,12 @@ def main():
             ghz = None
             if ts[7] > ts[0] > 0 and v[43] > v[42]:
                 ghz = round((v[43] - v[42]) / ((ts[7] - ts[0]) * 10.0), 2)  # cycles / ns
+            w0 = v[16:22]
+            wph = [round((w0[i + 1] - w0[i]) / 100.0, 2) if w0[i + 1] >= w0[i] > 0 else None for i in range(5)]
+            t0 = min(x for x in (v[16], v[32]) if x) if (v[16] or v[32]) else 0
+            arr = [round((x - t0) / 100.0, 2) if x and t0 else None for x in v[24:27]]
             print(json.dumps({"it": it, "paths": v[48:52], "ranker0_phase_us": ph, "Wk_P_W_fl": v[44:48],
-                              "clock_GHz": ghz}), flush=True)
+                              "worker0_phase_us": wph, "arrive_w0_r0_last_us": arr, "last_role": v[27]}), flush=True)
     comp.check_device()
 
 
