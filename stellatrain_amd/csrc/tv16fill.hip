@@ -453,7 +453,7 @@ tv16_fill(Tv16FillArgs A) {
         if (tid == 0 && (rep & (LF_RANKED | LF_FALLBACK)))
             atomicAdd(&A.dbg[48 + (ranked ? ((rep & LF_TIES) ? 1 : 0) : ((rep & LF_FALLBACK) ? 3 : 2))], 1u);
         if (ranked) return;
-        __syncthreads();  // the orderer's LDS view goes over the lfin view
+        lfin_list(Lf);  // the orderer's input (its LDS view then goes over the lfin view)
     }
     const uint32_t b = LONE ? 0u : blockIdx.x;  // a lone launch has one bucket
     uint32_t nst = 0;

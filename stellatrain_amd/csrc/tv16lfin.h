@@ -91,7 +91,7 @@ constexpr uint32_t LF_RANKED = 8u;    // a regime-B call the rankers took
 #ifndef STG_FILL_STAMPS
 #define STG_FILL_STAMPS 0
 #endif
-// diagnostics (STG_FILL_STAMPS builds): ranker 0's phase stamps, words 32..47;
+// diagnostics (STG_FILL_STAMPS builds): a ranker's phase stamps, words 32..41 (its clock 28, 29);
 // worker 0's, words 16..23
 #define LF_WSTAMP(i)                                                                                 \
     do {                                                                                             \
@@ -110,7 +110,7 @@ constexpr uint32_t LF_RANKED = 8u;    // a regime-B call the rankers took
 // What every lfin workgroup decides, identically.
 struct LfinDec {
     uint32_t Qtot, Wtot, kb, r, lim, c0, ct, cnt, M, N;
-    bool regimeB, tail_cand, listw, lists_ok;
+    bool regimeB, tail_cand, listw, lists_ok, any_big;  // any_big: a chunk lists more than LF_SPEC lines
     float t, inc, tail_key;
 };
 
@@ -125,7 +125,7 @@ __device__ __forceinline__ void lfin_prefix(LfinLds &L, const LfinArgs &A, LfinD
     float tv[16];
 #pragma unroll
     for (uint32_t i = 0; i < 16; ++i) tv[i] = i < d.tl ? d.src[(size_t)d.nb * 16 + i] : 0.f;
-    uint32_t qv[PER], wv[PER], sq = 0, sw = 0, bad = 0;
+    uint32_t qv[PER], wv[PER], sq = 0, sw = 0, bad = 0, big = 0;
 #pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
         const uint32_t c = tid * PER + u;
@@ -138,6 +138,7 @@ __device__ __forceinline__ void lfin_prefix(LfinLds &L, const LfinArgs &A, LfinD
         sq += qv[u];
         sw += wv[u];
         bad |= (qv[u] > LQCAP || wv[u] > LWCAP) ? 1u : 0u;
+        big |= qv[u] > 16u ? 1u : 0u;
     }
     D.t = A.cp->t;
     D.inc = A.cp->inc;
@@ -152,6 +153,7 @@ __device__ __forceinline__ void lfin_prefix(LfinLds &L, const LfinArgs &A, LfinD
     }
     if (tid == 0) { L.qp[nc] = D.Qtot; L.wp[nc] = D.Wtot; }
     D.lists_ok = !__syncthreads_or((int)bad);
+    D.any_big = __syncthreads_or((int)big);
     const uint32_t Qtot = D.Qtot;
     D.kb = d.dst_len / 16;
     D.r = d.dst_len % 16;
@@ -211,94 +213,80 @@ __device__ __forceinline__ void lfin_rescan(LfinLds &L, const Tv16FillBucket &d,
 }
 
 // ---------------------------------------------------------------------------
-// worker `wk`
+// worker `wk`: the qualifying lines of its chunks, loaded with the counts
 // ---------------------------------------------------------------------------
+constexpr uint32_t LF_SPEC = 16;  // list slots per chunk loaded before the counts are known
+__device__ __forceinline__ void lfin_store(const Tv16FillBucket &d, bool vec, uint32_t g, uint32_t kb, uint32_t r,
+                                           uint32_t line, float4 x, uint32_t q) {
+    const uint32_t len = g == kb ? r : 16u, off = 16 * g + 4 * q, pos = line * 16 + 4 * q;
+    const uint32_t bi = pos + (uint32_t)d.idx_offset;
+    if (vec && len == 16) {
+        *reinterpret_cast<float4 *>(d.val + off) = x;
+        *reinterpret_cast<uint4 *>(d.idx + off) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+    } else {
+        const float xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (uint32_t cc = 0; cc < 4; ++cc)
+            if (4 * q + cc < len) {
+                d.val[off + cc] = xs[cc];
+                d.idx[off + cc] = bi + cc;
+            }
+    }
+}
+
 __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
     const LfinArgs &A = L.args;
     const Tv16FillBucket &d = A.d;
     const uint32_t tid = threadIdx.x, nc = A.nc, nwk = A.workers;
-    LfinDec D;
     LF_WSTAMP(0);
+    // ---- its chunks' first LF_SPEC listed lines (position, data), in flight
+    //      with the counts: a lane per quarter line ----
+    const uint32_t pc = (nc + nwk - 1) / nwk, c_lo = min(nc, wk * pc), c_hi = min(nc, c_lo + pc);
+    constexpr uint32_t NS = 4;  // speculative quarter lines per thread
+    const uint32_t nspec = min((c_hi - c_lo) * LF_SPEC * 4, NS * FILL_WG);
+    uint32_t ls[NS];
+    float4 xs[NS];
+#pragma unroll
+    for (uint32_t i = 0; i < NS; ++i) {
+        const uint32_t t = tid + i * FILL_WG, c = c_lo + t / (LF_SPEC * 4), sl = (t / 4) % LF_SPEC;
+        if (t < nspec) {
+            ls[i] = A.lq[(size_t)c * LQCAP + sl];
+            xs[i] = A.lv[((size_t)c * LQCAP + sl) * 4 + (t & 3u)];
+        }
+    }
+    LfinDec D;
     lfin_prefix(L, A, D);
     LF_WSTAMP(1);
-    const uint32_t *qp = L.qp, *wp = L.wp;
+    const uint32_t *qp = L.qp;
     const bool vec = aligned16(d);
-    // ---- this worker's share of the qualifying lines, by global rank; a map
-    //      rank -> chunk built by one thread per chunk, then every line's two
-    //      loads (its position, its staged data) in flight together ----
-    const uint32_t nq = min(D.Qtot, D.lim);
-    const uint32_t per = (nq + nwk - 1) / nwk, g0 = min(nq, wk * per), g1 = min(nq, g0 + per);
-    for (uint32_t p0 = g0; p0 < g1; p0 += LF_QMAP) {
-        const uint32_t p1 = min(g1, p0 + LF_QMAP);
-        const uint32_t ca = chunk_of(qp, nc, p0), cb = chunk_of(qp, nc, p1 - 1);
-        for (uint32_t c = ca + tid; c <= cb; c += FILL_WG) {
-            const uint32_t a = max(qp[c], p0), b = min(qp[c + 1], p1);
-            for (uint32_t g = a; g < b; ++g) L.u.w.qmap[g - p0] = (uint16_t)c;
-        }
-        __syncthreads();
-        const uint32_t q = tid & 3u;
-        constexpr uint32_t KQ = 4;  // rounds of lines in flight together
-        for (uint32_t gb = p0 + (tid >> 2); gb < p1; gb += KQ * (FILL_WG / 4)) {
-            uint32_t pos[KQ], g[KQ];
-            float4 x[KQ];
 #pragma unroll
-            for (uint32_t k = 0; k < KQ; ++k) {
-                g[k] = gb + k * (FILL_WG / 4);
-                pos[k] = NONE;
-                if (g[k] < p1) {
-                    const uint32_t c = L.u.w.qmap[g[k] - p0], rr = g[k] - qp[c];
-                    if (qp[c + 1] - qp[c] <= LQCAP) {  // an overflowed chunk is re-read below
-                        pos[k] = (c * LCHUNK + A.lq[(size_t)c * LQCAP + rr]) * 16 + 4 * q;
-                        x[k] = A.lv[((size_t)c * LQCAP + rr) * 4 + q];
-                    }
-                }
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < KQ; ++k) {
-                if (pos[k] == NONE) continue;
-                const uint32_t len = g[k] == D.kb ? D.r : 16u, off = 16 * g[k] + 4 * q;
-                const uint32_t bi = pos[k] + (uint32_t)d.idx_offset;
-                if (vec && len == 16) {
-                    *reinterpret_cast<float4 *>(d.val + off) = x[k];
-                    *reinterpret_cast<uint4 *>(d.idx + off) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
-                } else {
-                    const float xs[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
-#pragma unroll
-                    for (uint32_t cc = 0; cc < 4; ++cc)
-                        if (4 * q + cc < len) {
-                            d.val[off + cc] = xs[cc];
-                            d.idx[off + cc] = bi + cc;
-                        }
-                }
-            }
-        }
-        __syncthreads();
+    for (uint32_t i = 0; i < NS; ++i) {
+        const uint32_t t = tid + i * FILL_WG, c = c_lo + t / (LF_SPEC * 4), sl = (t / 4) % LF_SPEC;
+        if (t >= nspec) continue;
+        const uint32_t qc = qp[c + 1] - qp[c], g = qp[c] + sl;
+        if (qc <= LQCAP && sl < qc && g < D.lim) lfin_store(d, vec, g, D.kb, D.r, c * LCHUNK + ls[i], xs[i], t & 3u);
     }
     LF_WSTAMP(2);
-    // ---- regime B: this worker's share of the window list, in scan order
-    //      (the exact orderer's input), one thread per (chunk, slot) ----
-    uint32_t *cu = const_cast<uint32_t *>(d.cand), *cl = cu + CAND_CAP, *ci = cu + 2 * CAND_CAP;
-    const uint32_t pc = (nc + nwk - 1) / nwk, c_lo = min(nc, wk * pc), c_hi = min(nc, c_lo + pc);
-    if (D.listw) {
-        for (uint32_t p = tid; p < (c_hi - c_lo) * LWCAP; p += FILL_WG) {
-            const uint32_t c = c_lo + p / LWCAP, i = p % LWCAP;
-            const uint32_t wc = wp[c + 1] - wp[c];
-            if (i >= wc || wc > LWCAP || qp[c + 1] - qp[c] > LQCAP) continue;  // overflowed: re-read below
-            const uint2 x = A.lw[(size_t)c * LWCAP + i];
-            const uint32_t line = c * LCHUNK + (x.y & 0xffffu), e = wp[c] + i;
-            st_sc1(&cu[e], x.x);
-            st_sc1(&cl[e], line * 16);
-            st_sc1(&ci[e], line - (qp[c] + (x.y >> 16)));
+    // ---- the rest: slots past the speculative ones (chunks with more listed
+    //      lines, or more chunks than the speculation covered) ----
+    static_assert(LF_SPEC == 16, "lfin_prefix flags chunks with more than 16 listed lines");
+    const uint32_t covered = nspec / (LF_SPEC * 4);  // chunks whose first LF_SPEC slots were taken
+    for (uint32_t c = c_lo + (D.any_big ? 0u : covered); c < c_hi; ++c) {
+        const uint32_t qc = qp[c + 1] - qp[c], s0 = c - c_lo < covered ? LF_SPEC : 0u;
+        if (qc > LQCAP || qc <= s0 || qp[c] + s0 >= D.lim) continue;  // overflowed (re-read below), or done
+        for (uint32_t t = s0 * 4 + tid; t < qc * 4; t += FILL_WG) {
+            const uint32_t sl = t / 4, g = qp[c] + sl;
+            if (g >= D.lim) continue;
+            lfin_store(d, vec, g, D.kb, D.r, c * LCHUNK + A.lq[(size_t)c * LQCAP + sl],
+                       A.lv[((size_t)c * LQCAP + sl) * 4 + (t & 3u)], t & 3u);
         }
     }
     LF_WSTAMP(3);
-    // ---- this worker's chunks whose lists overflowed: read again ----
+    // ---- its chunks whose lists overflowed: read again ----
     if (!D.lists_ok) {
         for (uint32_t c = c_lo; c < c_hi; ++c) {
-            const uint32_t qc = qp[c + 1] - qp[c], wc = wp[c + 1] - wp[c];
-            const bool emit = qc > LQCAP && qp[c] < D.lim;
-            const bool list = D.listw && wc && (wc > LWCAP || qc > LQCAP);
-            if (emit || list) lfin_rescan(L, d, c, D, emit, list);
+            const uint32_t qc = qp[c + 1] - qp[c];
+            if (qc > LQCAP && qp[c] < D.lim) lfin_rescan(L, d, c, D, true, false);
         }
     }
     LF_WSTAMP(4);
@@ -330,6 +318,37 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
     LF_WSTAMP(5);
 }
 
+// The exact orderer's input, by the last workgroup when it has to order the
+// fill itself: the window list in scan order (sum bits, position, candidate
+// index), from the scan's lists or, for a chunk whose lists overflowed, from src.
+__device__ __noinline__ void lfin_list(LfinLds &L) {
+    const LfinArgs &A = L.args;
+    const Tv16FillBucket &d = A.d;
+    const uint32_t tid = threadIdx.x, nc = A.nc;
+    LfinDec D;
+    lfin_prefix(L, A, D);
+    if (!D.listw) return;
+    uint32_t *cu = const_cast<uint32_t *>(d.cand), *cl = cu + CAND_CAP, *ci = cu + 2 * CAND_CAP;
+    const uint32_t *qp = L.qp, *wp = L.wp;
+    for (uint32_t p = tid; p < nc * LWCAP; p += FILL_WG) {
+        const uint32_t c = p / LWCAP, i = p % LWCAP;
+        const uint32_t wc = wp[c + 1] - wp[c];
+        if (i >= wc || wc > LWCAP || qp[c + 1] - qp[c] > LQCAP) continue;  // overflowed: re-read below
+        const uint2 x = A.lw[(size_t)c * LWCAP + i];
+        const uint32_t line = c * LCHUNK + (x.y & 0xffffu), e = wp[c] + i;
+        st_sc1(&cu[e], x.x);
+        st_sc1(&cl[e], line * 16);
+        st_sc1(&ci[e], line - (qp[c] + (x.y >> 16)));
+    }
+    if (!D.lists_ok)
+        for (uint32_t c = 0; c < nc; ++c) {
+            const uint32_t qc = qp[c + 1] - qp[c], wc = wp[c + 1] - wp[c];
+            if (wc && (wc > LWCAP || qc > LQCAP)) lfin_rescan(L, d, c, D, false, true);
+        }
+    vm_drain();
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // ranker `rk`: the regime-B fill's order for a share of the kept lines
 // ---------------------------------------------------------------------------
@@ -344,7 +363,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
     const uint32_t tid = threadIdx.x, nc = A.nc;
     LfinDec D;
     LF_STAMP(0);
-    if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[42] = (uint32_t)__builtin_amdgcn_s_memtime();  // the shader clock
+    if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[28] = (uint32_t)__builtin_amdgcn_s_memtime();  // the shader clock
     lfin_prefix(L, A, D);
     LF_STAMP(1);
     if (!D.regimeB || (!D.M && !D.tail_cand)) return;  // nothing to fill
@@ -368,6 +387,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         for (uint32_t e = L.wp[c]; e < L.wp[c + 1]; ++e) L.u.r.emap[e] = (uint16_t)c;
     for (uint32_t i = tid; i < NBIN; i += FILL_WG) L.bin[i] = 0;
     __syncthreads();
+    LF_STAMP(2);
     constexpr uint32_t KW = CAND_CAP / FILL_WG;  // entries per thread: e = tid + k * FILL_WG
     static_assert(KW * FILL_WG == CAND_CAP, "window entries per thread");
     uint32_t ok[KW], cx[KW], ln[KW];
@@ -401,7 +421,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         }
     }
     __syncthreads();
-    LF_STAMP(2);
+    LF_STAMP(3);
     // ---- keep the first bins holding M + 2 entries: every pop, the first
     //      line past them and its ties (a bin never splits equal sums) ----
     {
@@ -424,7 +444,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
         return;
     }
-    LF_STAMP(3);
+    LF_STAMP(4);
     // ---- the kept lines, compacted from registers, and grouped by bin ----
     uint32_t *const kk = L.u.r.kk, *const kc = L.u.r.kc, *const kr = L.u.r.kr, *const kl = L.u.r.kl;
     {
@@ -451,7 +471,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         }
         __syncthreads();
     }
-    LF_STAMP(4);
+    LF_STAMP(5);
     // order: (key desc, right-first pre-order of the start position asc)
     auto before = [&](uint32_t f, uint32_t e) { return kk[f] > kk[e] || (kk[f] == kk[e] && kr[f] < kr[e]); };
     auto rank_of = [&](uint32_t e) {  // its bin's start + the bin's lines before it
@@ -499,7 +519,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         }
         __syncthreads();
     }
-    LF_STAMP(5);
+    LF_STAMP(6);
     const uint32_t KH = L.kh;  // R: the kept lines with key >= KH
     const uint32_t late = D.N > Ph + 1 ? D.N - (Ph + 1) : 0u;  // start positions >= late: the last Ph + 1
     // ---- this ranker's share: a thread per line, its rank within its bin;
@@ -527,6 +547,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         }
     }
     __syncthreads();
+    LF_STAMP(7);
     {   // (3): no line of R at a late line's parent or sibling -- every thread
         // takes its kept lines against every late one
         const uint32_t nl = L.nlate;
@@ -541,7 +562,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
                 }
             }
     }
-    LF_STAMP(6);
+    LF_STAMP(8);
     // ---- emit the share's pops: four lanes per line ----
     const bool vec = aligned16(d) && (D.cnt & 3u) == 0;
     auto offset = [&](uint32_t i) { return 16u * i - (tr < i ? 16u - d.tl : 0u); };
@@ -565,6 +586,6 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
     const bool viol = __syncthreads_or((int)(fl & LF_VIOL));
     if (tid == 0 && (viol || ties)) g_or(&A.cc->pad[5], (ties ? LF_TIES : 0u) | (viol ? LF_VIOL : 0u));
     if (STG_FILL_STAMPS && rk == STG_FILL_STAMPS_RK && tid == 0) { A.dbg[44] = Wk; A.dbg[45] = P; A.dbg[46] = s1 - s0; A.dbg[47] = fl; }
-    LF_STAMP(7);
-    if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[43] = (uint32_t)__builtin_amdgcn_s_memtime();
+    LF_STAMP(9);
+    if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[29] = (uint32_t)__builtin_amdgcn_s_memtime();
 }

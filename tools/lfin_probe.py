@@ -42,9 +42,9 @@ def main():
         if it >= nk:  # steady state: one stamp line per call
             check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
             v = list(w)
-            ts = v[32:40]
+            ts = v[32:42]
             # a phase a call did not reach keeps an earlier call's stamp: only increasing ones count
-            ph = [round((ts[i + 1] - ts[i]) / 100.0, 2) if ts[i + 1] >= ts[i] > 0 else None for i in range(7)]
+            ph = [round((ts[i + 1] - ts[i]) / 100.0, 2) if ts[i + 1] >= ts[i] > 0 else None for i in range(9)]
             ghz = None
             if ts[7] > ts[0] > 0 and v[43] > v[42]:
                 ghz = round((v[43] - v[42]) / ((ts[7] - ts[0]) * 10.0), 2)  # cycles / ns
@@ -52,8 +52,10 @@ def main():
             wph = [round((w0[i + 1] - w0[i]) / 100.0, 2) if w0[i + 1] >= w0[i] > 0 else None for i in range(5)]
             t0 = min(x for x in (v[16], v[32]) if x) if (v[16] or v[32]) else 0
             arr = [round((x - t0) / 100.0, 2) if x and t0 else None for x in v[24:27]]
-            print(json.dumps({"it": it, "paths": v[48:52], "ranker0_phase_us": ph, "Wk_P_W_fl": v[44:48],
-                              "worker0_phase_us": wph, "arrive_w0_r0_last_us": arr, "last_role": v[27]}), flush=True)
+            ghz = round(((v[29] - v[28]) & 0xffffffff) / ((ts[9] - ts[0]) * 10.0), 2) if ts[9] > ts[0] > 0 else None
+            print(json.dumps({"it": it, "paths": v[48:52], "ranker_phase_us": ph, "Wk_P_share_fl": v[44:48],
+                              "worker0_phase_us": wph, "arrive_w0_r0_last_us": arr, "last_role": v[27],
+                              "ranker_clock_GHz": ghz}), flush=True)
     comp.check_device()
 
 

@@ -11,5 +11,6 @@ run() {  # name env...
     grep single "gpurun_out/sw_$name.log" >> gpurun_out/sweep.txt
     python3 tools/ktrace.py "gpurun_out/sw_$name" | grep tv16 >> gpurun_out/sweep.txt
 }
-run default STG_X=1 && run r0 STG_TV16_LFIN_RANKERS=0 && run w16 STG_TV16_LFIN_WORKERS=16 && \
-run w128 STG_TV16_LFIN_WORKERS=128 && run r8 STG_TV16_LFIN_RANKERS=8 && run old STG_TV16_LFIN=0
+for v in ${SWEEP:-"default:STG_X=1" "shape1:STG_TV16_LSHAPE=1" "w32:STG_TV16_LFIN_WORKERS=32" "r16:STG_TV16_LFIN_RANKERS=16"}; do
+    run "${v%%:*}" "${v#*:}" || break
+done
