@@ -15,14 +15,17 @@ Cache); step s compresses set s%2, so every key sees fresh data each visit and
 its AIMD threshold runs its real regime A/B sequence.  Keys are initialised
 (first-threshold call) before the warmup.  value = 16 x 64 MiB x steps / time.
 
-N > 1 (BASELINE.json configs[3]): the 1,024-bucket stream (256 KiB - 64 MiB,
-log-uniform, seeded: shard.c4_sizes) sharded over the N ranks by
-shard.ShardPlan (key-affine, bytes-balanced).  Buckets are independent
-(core.cpp:1052-1087), so each rank compresses its own buckets with no
-collective on the data path; one step = one sweep over the rank's buckets in
-batched launches of <= 16 on four streams.  The whole list is fixed, so this is
-strong scaling; value = all ranks' bytes / the slowest rank's time.  RCCL is
-used only for the timing barrier and the max-reduce of the elapsed time.
+N > 1: the same step on every rank (each its own 16 keys and buckets, seeded
+by rank): buckets are independent (core.cpp:1052-1087), so the path shards
+with no collective; "scaling": "weak", value = all ranks' bytes / the slowest
+rank's time, and per_rank_GBps lists each rank's rate.
+
+Every N also carries a ``c4`` sub-object (BASELINE.json configs[3]): the
+1,024-bucket stream (256 KiB - 64 MiB, log-uniform, seeded: shard.c4_sizes)
+sharded over the N ranks by shard.ShardPlan (key-affine, bytes-balanced), one
+sweep = every bucket once in batched launches of <= 16 on four streams; the
+list is fixed, so that is strong scaling (N = 1 runs the whole stream on one
+GPU).  RCCL carries only the timing barriers and the max / sum reductions.
 
 ``--gpus N`` with N > 1 outside torchrun relaunches this script under
 ``torch.distributed.run`` (one process per GPU) before any GPU call.
@@ -30,9 +33,12 @@ used only for the timing barrier and the max-reduce of the elapsed time.
 restatement stands in for the device; small sizes) for tests/test_bench_cli.py.
 
 Extra fields: ``roofline`` for the dominant (only) kernel, tv16_batch, timed
-live with HIP events over the profiled steps (algorithmic bytes = 4n + 8k per
-bucket; avg_us = the uninstrumented per-launch duration, concurrent launches x
-interval / launches); ``cpu_baseline`` (rank 0 at N = 1): the reference's own
+live with HIP events over the profiled steps on stream 0, the other streams
+joined to it (algorithmic bytes = 4n + 8k per bucket; achieved = those bytes
+over the interval; pitch_us = interval x concurrent launches / launches, the
+per-launch share of the chip's time -- launches overlap, so rocprofv3's
+per-launch duration is longer than the pitch by the overlap factor);
+``cpu_baseline`` (rank 0 at N = 1): the reference's own
 backend/src/compress build (oracle/_ref, kind "reference") or the restatement
 (kind "port"), timed on this host on 1 thread and on T = min(cpus, 32) threads
 with distinct keys, as the engine's pool runs them (config.h:7).
@@ -66,7 +72,8 @@ def parse():
     p.add_argument("--keys", type=int, default=16)
     p.add_argument("--method", default="thresholdv16")
     p.add_argument("--workload", choices=["auto", "headline", "c4"], default="auto",
-                   help="auto: the 64 MiB headline at N = 1, the sharded C4 stream at N > 1")
+                   help="the main line's workload (auto: the 64 MiB headline at every N; c4: the C4 stream)")
+    p.add_argument("--c4-sweeps", type=int, default=3, help="timed sweeps of the c4 sub-object (0: none)")
     p.add_argument("--c4-count", type=int, default=1024)
     p.add_argument("--c4-lo", type=int, default=65536)
     p.add_argument("--c4-hi", type=int, default=16777216)
@@ -182,7 +189,7 @@ def workload(args, world, rank):
     from stellatrain_amd.shard import ShardPlan, c4_sizes
     wl = args.workload
     if wl == "auto":
-        wl = "headline" if world == 1 else "c4"
+        wl = "headline"
     if wl == "headline":
         n = args.mib * (1 << 20) // 4
         ids = list(range(args.keys))
@@ -200,6 +207,88 @@ def workload(args, world, rank):
                         f"ShardPlan; step = one sweep", "buckets": len(sizes), "bytes_total": 4 * sum(sizes),
             "imbalance": round(plan.imbalance(), 5)}
     return wl, items, desc, {r: plan.local(r) for r in range(world)}
+
+
+def c4_measure(args, world, rank, comp, streams, dist):
+    """The c4 sub-object: this rank's ShardPlan share of the C4 stream, two
+    buffer sets, one sweep = every bucket once (batches of <= 16 distinct keys,
+    batch j on stream j % S); max over ranks of the timed sweeps."""
+    import ctypes as C
+
+    import torch
+    from stellatrain_amd._capi import check, lib
+    from stellatrain_amd.engine import merge_numel
+    from stellatrain_amd.shard import ShardPlan, c4_sizes
+    from stellatrain_amd.synth import seed_for
+    dev = streams[0].device
+    sizes = c4_sizes(args.c4_count, args.c4_lo, args.c4_hi)
+    plan = ShardPlan(sizes, world)
+    mine = plan.local(rank)
+    ns = len(streams)
+    tot = sum(sizes[b] for b in mine)
+    offs = np.concatenate([[0], np.cumsum([sizes[b] for b in mine])]).astype(np.int64)
+    ks = [merge_numel(sizes[b], args.ratio, 1) for b in mine]
+    koffs = np.concatenate([[0], np.cumsum(ks)]).astype(np.int64)
+    sets = [torch.empty(max(tot, 1), dtype=torch.float32, device=dev) for _ in range(2)]
+    for par in range(2):
+        for j, b in enumerate(mine):
+            check(lib().stg_synth_fill_device(C.c_void_p(sets[par][offs[j]:].data_ptr()), sizes[b], seed_for(b, par),
+                                              0, 0, C.c_void_p(streams[0].cuda_stream)))
+    oidx = torch.zeros(max(sum(ks), 1), dtype=torch.int32, device=dev)
+    oval = torch.zeros(max(sum(ks), 1), dtype=torch.float32, device=dev)
+    counts = torch.zeros(max(len(mine), 1), dtype=torch.int32, device=dev)
+    groups = [list(range(j, min(j + 16, len(mine)))) for j in range(0, len(mine), 16)]
+    plans = []
+    for par in range(2):
+        calls = []
+        for j, g in enumerate(groups):
+            rows = [(plan.key(mine[i]).encode(), sets[par][offs[i]:].data_ptr(), sizes[mine[i]], ks[i],
+                     oidx[koffs[i]:].data_ptr(), ks[i], oval[koffs[i]:].data_ptr(), counts.data_ptr() + 4 * i)
+                    for i in g]
+            calls.append((comp.bucket_array(rows), len(rows), streams[j % ns].cuda_stream))
+        plans.append(calls)
+
+    def sweep(s):
+        for arr, n_, sp in plans[s % 2]:
+            comp.compress_batch_raw(arr, n_, sp)
+
+    def sync():
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
+        torch.cuda.synchronize()
+    for s in range(3):  # first calls (first thresholds) and warm-up
+        sweep(s)
+    sync()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.c4_sweeps):
+        sweep(s)
+    sync()
+    el = time.perf_counter() - t0
+    comp.check_device()
+    assert bool((counts[:len(mine)].cpu().numpy() == np.array(ks, np.int32)).all()), "count != dst_len"
+    my = torch.tensor([el, 4.0 * tot], dtype=torch.float64, device=dev)
+    per_rank = [None] * world
+    if world > 1:
+        ts = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(ts, my)
+        per_rank = [(float(t[0]), float(t[1])) for t in ts]
+    else:
+        per_rank = [(el, 4.0 * tot)]
+    slow = max(e for e, _ in per_rank)
+    total = sum(b for _, b in per_rank)
+    return {"workload": f"C4: stream of {len(sizes)} {args.method} buckets k=1% ({args.c4_lo * 4 >> 10} KiB - "
+                        f"{args.c4_hi * 4 >> 20} MiB, log-uniform, seeded) sharded over {world} GPU(s) by ShardPlan; "
+                        "one sweep = every bucket once", "scaling": "strong", "buckets": len(sizes),
+            "bytes_per_sweep": int(total), "sweeps": args.c4_sweeps,
+            "value": round(total * args.c4_sweeps / slow / 1e9, 2), "unit": "GB/s",
+            "ms_per_sweep": round(slow * 1e3 / args.c4_sweeps, 4),
+            "per_rank_GBps": [round(b * args.c4_sweeps / e / 1e9, 2) for e, b in per_rank],
+            "per_rank_buckets": [len(plan.local(r)) for r in range(world)],
+            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
+            "imbalance": round(plan.imbalance(), 5)}
 
 
 def spawn_ranks(args):
@@ -312,6 +401,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    el_mine = el
     tt = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -339,12 +429,16 @@ def main():
     chip_ms = ev0.elapsed_time(ev1)
     launches = args.profile_steps * len(groups)
     conc = min(ns, len(groups))
-    avg_us = chip_ms * 1e3 * conc / max(launches, 1)
+    pitch_us = chip_ms * 1e3 * conc / max(launches, 1)
 
     my_bytes = 4.0 * tot
     all_bytes = torch.tensor([my_bytes], dtype=torch.float64, device=dev)
+    per_rank_gbps = [round(my_bytes * args.steps / el_mine / 1e9, 2)]
     if world > 1:
         dist.all_reduce(all_bytes)
+        rates = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(rates, torch.tensor([my_bytes * args.steps / el_mine / 1e9], dtype=torch.float64, device=dev))
+        per_rank_gbps = [round(float(r.item()), 2) for r in rates]
     total_bytes = float(all_bytes.item()) * args.steps
     value = total_bytes / el / 1e9
     alg_step = sum(4.0 * n + 8.0 * k for _, n, k, _ in items)  # 4n + 8k per bucket
@@ -354,6 +448,11 @@ def main():
         gathered = [None] * world
         dist.all_gather_object(gathered, {"rank": rank, "buckets": [b for *_, b in items], "bytes": my_bytes})
         shard_meta = gathered
+    c4 = None
+    if wl == "headline" and args.c4_sweeps > 0:
+        del sets
+        torch.cuda.empty_cache()
+        c4 = c4_measure(args, world, rank, comp, streams, dist)
     if rank == 0:
         per_launch = nb / max(len(groups), 1)
         out = {
@@ -376,9 +475,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(per_launch) if wl == "headline" else None,
                          "kernel": "tv16_batch", "alg_bytes_per_launch": int(alg_step / max(len(groups), 1)),
-                         "avg_us": round(avg_us, 2), "concurrent_launches": conc, "launches_timed": int(launches),
+                         "pitch_us": round(pitch_us, 2), "concurrent_launches": conc, "launches_timed": int(launches),
                          "interval_us": round(chip_ms * 1e3, 1), "rank": 0},
             "per_gpu_GBps": round(value / world, 2),
+            "per_rank_GBps": per_rank_gbps,
+            "rccl_world_size": dist.get_world_size() if world > 1 else 1,
             "per_bucket_us": round(el * 1e6 / (args.steps * nb), 3),
             "first_call_ms": round(first_ms, 3),
             "host_enqueue_us_per_step": round(t_enq * 1e6 / args.steps, 2),
@@ -388,6 +489,8 @@ def main():
                              for g in shard_meta]
             if args.dump_shards:
                 json.dump(shard_meta, open(args.dump_shards, "w"))
+        if c4 is not None:
+            out["c4"] = c4
         if world == 1 and not args.no_cpu_baseline and wl == "headline":
             out["cpu_baseline"] = cpu_baseline(items[0][1], items[0][2], args.cpu_seconds)
         print(json.dumps(out), flush=True)
@@ -398,48 +501,71 @@ def main():
 
 def main_oracle(args, world, rank):
     """CPU rehearsal of the rank layout (tests): gloo, the restatement standing
-    in for the device, the same workload / ShardPlan / timing / reduction."""
+    in for the device, the same workloads (the headline per rank, the c4
+    sub-object's ShardPlan shares), timing and reductions."""
     import torch
     import torch.distributed as dist
     from oracle.oracle import Oracle
+    from stellatrain_amd.engine import merge_numel
+    from stellatrain_amd.shard import ShardPlan, c4_sizes
     from stellatrain_amd.synth import seed_for
     if world > 1:
         dist.init_process_group("gloo", init_method="env://")
     wl, items, desc, _ = workload(args, world, rank)
     o = Oracle()
     h = o.tv16_new()
-    data = [[o.synth(n, seed_for(b, par)) for (_, n, _, b) in items] for par in range(2)]
 
-    def step(s):
-        return [o.tv16_compress(h, key, data[s % 2][j], k)[0] for j, (key, _, k, _) in enumerate(items)]
-    step(0)
-    for s in range(args.warmup):
-        step(s + 1)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        cnt = step(s)
-    if world > 1:
-        dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    my_bytes = torch.tensor([4.0 * sum(n for _, n, _, _ in items)], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        dist.all_reduce(my_bytes)
-    assert cnt == [k for _, _, k, _ in items]
-    gathered = [{"rank": rank, "buckets": [b for *_, b in items]}]
-    if world > 1:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, {"rank": rank, "buckets": [b for *_, b in items]})
+    def timed(items_, steps):
+        data = [[o.synth(n, seed_for(b, par)) for (_, n, _, b) in items_] for par in range(2)]
+
+        def step(s):
+            return [o.tv16_compress(h, key, data[s % 2][j], k)[0] for j, (key, _, k, _) in enumerate(items_)]
+        step(0)
+        for s in range(args.warmup):
+            step(s + 1)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        cnt = None
+        for s in range(steps):
+            cnt = step(s)
+        el = time.perf_counter() - t0
+        assert cnt == [k for _, _, k, _ in items_]
+        mine = torch.tensor([el, 4.0 * sum(n for _, n, _, _ in items_)], dtype=torch.float64)
+        if world > 1:
+            allr = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(allr, mine)
+        else:
+            allr = [mine]
+        slow = max(float(t[0]) for t in allr)
+        total = sum(float(t[1]) for t in allr)
+        return total * steps / slow / 1e9, slow, [round(float(t[1]) * steps / float(t[0]) / 1e9, 4) for t in allr]
+
+    value, slow, per_rank = timed(items, args.steps)
+    c4 = None
+    gathered = []
+    if wl == "headline" and args.c4_sweeps > 0:
+        sizes = c4_sizes(args.c4_count, args.c4_lo, args.c4_hi)
+        plan = ShardPlan(sizes, world)
+        c4_items = [(plan.key(b), sizes[b], merge_numel(sizes[b], args.ratio, 1), b) for b in plan.local(rank)]
+        c4_value, c4_slow, c4_rates = timed(c4_items, args.c4_sweeps)
+        c4 = {"scaling": "strong", "buckets": len(sizes), "value": round(c4_value, 4), "unit": "GB/s",
+              "ms_per_sweep": round(c4_slow * 1e3 / args.c4_sweeps, 3), "per_rank_GBps": c4_rates,
+              "per_rank_buckets": [len(plan.local(r)) for r in range(world)],
+              "rccl_world_size": dist.get_world_size() if world > 1 else 1}
+        gathered = [{"rank": rank, "buckets": plan.local(rank)}]
+        if world > 1:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, {"rank": rank, "buckets": plan.local(rank)})
     if rank == 0:
-        value = float(my_bytes.item()) * args.steps / float(el.item()) / 1e9
         out = {"metric": METRIC, "value": round(value, 4), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-               "warmup": args.warmup, "ms_per_step": round(float(el.item()) * 1e3 / args.steps, 3),
+               "warmup": args.warmup, "ms_per_step": round(slow * 1e3 / args.steps, 3),
                "higher_is_better": True, "scaling": "weak" if wl == "headline" else "strong", "vs_baseline": None,
                "dtype": "f32", "data": "synthetic (CPU rehearsal: oracle restatement standing in for the device)",
                "config": dict(desc, backend="oracle", parallelism=f"bucket-sharded x{world}, no collective"),
-               "shards": [{"rank": g["rank"], "buckets": len(g["buckets"])} for g in gathered]}
+               "per_rank_GBps": per_rank, "rccl_world_size": dist.get_world_size() if world > 1 else 1}
+        if c4 is not None:
+            out["c4"] = c4
         if args.dump_shards:
             json.dump(gathered, open(args.dump_shards, "w"))
         print(json.dumps(out), flush=True)

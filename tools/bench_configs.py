@@ -456,10 +456,76 @@ def gather(torch, calls):
     return out
 
 
+def cpu_codec(method, mib, ratio, seconds):
+    """The reference CPU path beside its GPU row, same run, this host's cores
+    (north_star): oracle/_ref/libstg_ref.so (the reference's compress/*.cpp
+    built in place, -O3 -march=broadwell) when it travelled, else the
+    restatement.  1 thread, then T = min(CPU share, 32) threads, each a codec
+    of its own (threshold-v: its own handle, the state keyed by the src
+    pointer, thresholdv.cpp:44) over 2 shared alternating synthetic buckets
+    (read-only for both codecs); steady-state calls (first calls excluded)."""
+    import threading
+    from oracle.oracle import REF_SO, Oracle, Reference
+    sys.path.insert(0, ROOT)
+    from bench import cpu_model, cpu_threads
+    from stellatrain_amd import merge_numel
+    o = Oracle()
+    kind = "reference" if os.path.exists(REF_SO) else "port"
+    impl = Reference() if kind == "reference" else o
+    n = mib * (1 << 20) // 4
+    k = merge_numel(n, ratio)
+    bufs = [o.synth(n, 0x5EED0000 + 77 * 1000 + s) for s in range(2)]
+    T = cpu_threads()
+
+    def run(nthreads, secs):
+        hs = [impl.tv_new() if method == "thresholdv" else None for _ in range(nthreads)]
+
+        def one(t, c):
+            if method == "thresholdv":
+                impl.tv_compress(hs[t], 1, bufs[c % 2], k)
+            elif kind == "reference":
+                impl.topk_compress(bufs[c % 2], k)
+            else:
+                impl.topk_compress(bufs[c % 2], k, bug_compat=True)
+        for t in range(nthreads):  # first call (threshold-v: nth_element over n) excluded
+            one(t, 1)
+        calls = [0] * nthreads
+        stop = time.perf_counter() + secs
+        barrier = threading.Barrier(nthreads + 1)
+
+        def worker(t):
+            barrier.wait()
+            c = 0
+            while time.perf_counter() < stop or c == 0:
+                one(t, c)
+                c += 1
+            calls[t] = c
+        ths = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+        for th in ths:
+            th.start()
+        t0 = time.perf_counter()
+        barrier.wait()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t0
+        for h in hs:
+            if h is not None:
+                impl.tv_free(h)
+        return 4.0 * n * sum(calls) / dt / 1e9, sum(calls), dt
+    v1, c1, d1 = run(1, seconds / 2)
+    vT, cT, dT = run(T, seconds / 2)
+    return {"config": f"CPU {method} {mib} MiB k={k} ({'reference build' if kind == 'reference' else 'restatement'})",
+            "kind": kind, "cpu": cpu_model(), "GBps_dense_in_1thread": round(v1, 3), "threads": T,
+            "GBps_dense_in_T": round(vT, 3),
+            "sample": f"{c1} calls in {d1:.1f} s on 1 thread, {cT} calls in {dT:.1f} s on {T} threads; 2 alternating "
+                      "synthetic buckets, first call excluded"}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--calls", type=int, default=48)
     p.add_argument("--c4-streams", type=int, default=4)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU baseline row (0: none)")
     p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,merge,ef,gather")
     a = p.parse_args()
     import torch
@@ -472,8 +538,12 @@ def main():
     for m, tag in (("topk", "c2"), ("topk_exact", "c2")):
         if tag in only or m in only:  # "topk" / "topk_exact": one mode alone (PMC passes)
             emit(time_device(torch, make_compressor(m), m, 64, 0.99, a.calls, 8, 9))
+    if "c2" in only and a.cpu_seconds > 0:  # the reference CPU path beside the GPU rows
+        emit(cpu_codec("topk", 64, 0.99, a.cpu_seconds))
     if "c3" in only or "c3dev" in only:
         emit(time_device(torch, make_compressor("thresholdv"), "thresholdv", 256, 0.999, a.calls, 8, 3))
+    if "c3" in only and a.cpu_seconds > 0:
+        emit(cpu_codec("thresholdv", 256, 0.999, a.cpu_seconds))
     if "c3" in only:
         emit(host_inclusive(torch, "thresholdv", 256, 0.999, 12))
     if "e2e" in only:
