@@ -44,6 +44,12 @@ using namespace tv16;
 #define STG_EF_AUX 2  // cache policy of the fused residual stores (2: nontemporal)
 #endif
 
+// diagnostics only (timing attribution; wrong results): 1 = no per-chunk
+// lists written, 2 = the plain stream (no line sums, no lists)
+#ifndef STG_LSCAN_DIAG
+#define STG_LSCAN_DIAG 0
+#endif
+
 struct LLds {
     float4 qv[2][LQCAP][4];  // their data (a float4 per lane of the line's quad)
     uint32_t ql[2][LQCAP];  // qualifying lines of the chunk in the slot (unordered)
@@ -153,6 +159,11 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
 #pragma unroll
             for (uint32_t u = 0; u < D; ++u) {
                 const float4 x = v[u];
+                if (STG_LSCAN_DIAG == 2) {
+                    v[u] = load(m0 + u + D);
+                    if (__float_as_uint(x.x + x.y + x.z + x.w) == 0x7f800001u) L.qn[sl] = 1;
+                    continue;
+                }
                 uint32_t ll = lane_line;
                 asm volatile("" : "+v"(ll));
                 const uint32_t i = (m0 + u) * (NW * 16u) + ll;  // line within the chunk
@@ -199,7 +210,15 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
         lds_drain();
         uint32_t old = 0;
         if (lane == 0) old = atomicAdd(&L.done[sl], 1u);
-        if (uni(old) == NW - 1) finalize(L, A, sl, c, j);  // every other wave's list adds were drained first
+        if (uni(old) == NW - 1) {  // every other wave's list adds were drained first
+            if (STG_LSCAN_DIAG) {
+                if (lane == 0) { L.qn[sl] = 0; L.wn[sl] = 0; L.done[sl] = 0; }
+                lds_drain();
+                if (lane == 0) lds_st(&L.fin[sl], j + 1);
+            } else {
+                finalize(L, A, sl, c, j);
+            }
+        }
     }
 }
 
