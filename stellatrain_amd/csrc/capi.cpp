@@ -106,6 +106,8 @@ struct Workspace {
         const size_t o_cand = carve(sizeof(uint32_t) * stg::CAND_WORDS * stg::MAX_BATCH);
         const size_t o_misc = carve(sizeof(uint32_t) * 64);
         const size_t o_tvt = carve(sizeof(uint64_t));
+        const size_t o_wh = carve(sizeof(uint32_t) * stg::LNBIN);
+        const size_t o_we = carve(sizeof(uint2) * stg::LNBIN * stg::LBCAP);
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
         // control block are ordered after it (a plain hipMemset runs on the
@@ -119,6 +121,8 @@ struct Workspace {
         d.cand = reinterpret_cast<uint32_t *>(b + o_cand);
         d.misc = reinterpret_cast<uint32_t *>(b + o_misc);
         d.tv_ticket = reinterpret_cast<uint64_t *>(b + o_tvt);
+        d.whist = reinterpret_cast<uint32_t *>(b + o_wh);
+        d.went = reinterpret_cast<uint2 *>(b + o_we);
         return STG_OK;
     }
 

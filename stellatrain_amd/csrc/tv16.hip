@@ -805,6 +805,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         L.lq = ws.lq;
         L.lw = ws.lw;
         L.lv = ws.lv;
+        L.whist = ws.whist;
+        L.went = ws.went;
         L.zero_next = reinterpret_cast<uint32_t *>(&ws.ctl->cc[(a.epoch + 1) & 1u]);
         hipError_t e = launch_tv16_lscan(L, a.num_cu, s);
         if (e != hipSuccess) return e;
@@ -825,7 +827,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             getenv("STG_TV16_LFIN_WORKERS") ? atoi(getenv("STG_TV16_LFIN_WORKERS")) : 64, 192));
         (void)helpers;
         static const uint32_t rankers = std::max(0, std::min(
-            getenv("STG_TV16_LFIN_RANKERS") ? atoi(getenv("STG_TV16_LFIN_RANKERS")) : 32, 128));
+            getenv("STG_TV16_LFIN_RANKERS") ? atoi(getenv("STG_TV16_LFIN_RANKERS")) : 8, 128));
         F.helpers = 0;
         F.cc = &ws.ctl->cc[a.epoch & 1u];
         F.lfin = true;
@@ -836,6 +838,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.lq = ws.lq;
         F.lw = ws.lw;
         F.lv = ws.lv;
+        F.whist = ws.whist;
+        F.went = ws.went;
         F.state = a.b[0].state;
         F.cp = ws.cp;
         F.resid = a.b[0].resid;

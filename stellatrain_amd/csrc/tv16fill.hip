@@ -424,6 +424,8 @@ tv16_fill(Tv16FillArgs A) {
             W.lq = A.lq;
             W.lw = A.lw;
             W.lv = A.lv;
+            W.whist = A.whist;
+            W.went = A.went;
             W.state = A.state;
             W.cp = A.cp;
             W.resid = A.resid;
@@ -445,6 +447,8 @@ tv16_fill(Tv16FillArgs A) {
             if (s_last) { A.dbg[26] = (uint32_t)__builtin_amdgcn_s_memrealtime(); A.dbg[27] = role; }
         }
         if (!s_last) return;
+        // every role is done with the binned window: zero its counts for the next call
+        for (uint32_t i = tid; i < LNBIN; i += FILL_WG) st_sc1(&A.whist[i], 0u);
         const uint32_t rep = ld_sc1(&A.cc->pad[5]);
         // how the call's fill was ordered (debug words 48..51: rankers without
         // ties, rankers with ties, the orderer after a violation, the orderer

@@ -17,12 +17,13 @@
 //            scan order (the exact orderer's input); worker 0 writes the
 //            ragged tail, the AIMD state, the count and the decision;
 //   rankers  (the next `rankers` tickets)  decide the same way; in regime B
-//            each loads the whole window list, keeps the top bins (the pops,
-//            the first line past them and its ties), ranks a balanced share
-//            of the kept lines by (sum desc, right-first pre-order of the
-//            start position) -- the pop order whenever the fill's fast paths
-//            hold (see tv16fill.hip (2), (3)) -- and writes them; it checks
-//            those conditions for its share and reports ties / violations;
+//            each reads the scan's window histogram (ws.h LNBIN bins of 256
+//            ulps below t), keeps the first bins (the pops, the first line
+//            past them and its ties), loads only those bins' entries (the scan
+//            stored them by bin), ranks every kept line by (sum desc,
+//            right-first pre-order of the start position) -- the pop order
+//            whenever the fill's fast paths hold (see tv16fill.hip (2), (3))
+//            -- checks those conditions, and emits its share of the pops;
 //   every workgroup then adds to one counter; the last one (every write of
 //            the others is in) runs the exact orderer of tv16fill.hip over the
 //            workers' window list when the rankers could not prove their
@@ -38,6 +39,8 @@ struct LfinArgs {
     const uint32_t *lq;
     const uint2 *lw;
     const float4 *lv;
+    uint32_t *whist;  // the scan's binned window: counts per bin, entries LBCAP per bin
+    const uint2 *went;
     KeyState *state;
     const CallParams *cp;
     float *resid;
@@ -51,25 +54,22 @@ struct LfinLds {
     uint32_t qp[LMAXC + 1];  // per chunk: exclusive prefix of qualifying lines (+ total)
     uint32_t wp[LMAXC + 1];  // ... of window lines
     union {
-        struct {                       // ranker
-            uint16_t emap[CAND_CAP];   // window entry -> its chunk
-            uint32_t kk[EMAX];         // kept lines: order key ford(line sum)
+        struct {                       // ranker: the kept window entries, grouped by bin
+            uint64_t kg[EMAX];         // sort key: window offset (bits(t) - 1 - bits(sum)) << 25 | right-first key
             uint32_t kc[EMAX];         // ... candidate index (start heap position)
-            uint32_t kr[EMAX];         // ... right-first pre-order key of the start position
             uint32_t kl[EMAX];         // ... line (the ragged tail: nb)
-            uint16_t bl2[EMAX];        // kept lines grouped by bin
-            uint16_t rr[EMAX];         // this ranker's share: rank of each
-            uint32_t cur[NBIN];        // bin cursors
+            uint16_t emap[EMAX];       // ... its bin
+            uint16_t ord[EMAX];        // rank -> kept entry
+            uint8_t tf[EMAX];          // ... LF_TIES / LF_VIOL if it turns out to be in R
         } r;
         struct {                       // worker: rank -> chunk
             uint16_t qmap[LF_QMAP];
         } w;
     } u;
-    uint32_t bin[NBIN];        // ranker: window histogram -> bin starts
+    uint32_t bin[NBIN + 1];    // ranker: kept entries of the bins before each bin (+ all)
     uint32_t sh[32];
-    uint32_t bl[64];           // the bin holding rank Ph: its kept keys
-    uint32_t late[64];         // this ranker's lines of R starting in the last Ph + 1 positions
-    uint32_t cut, wk, nbl, tail_e, tail_rank, kh, nlate;
+    uint32_t late[64];         // lines of R starting in the last Ph + 1 positions
+    uint32_t cut, wk, tail_rank, nlate;
     LfinArgs args;
 };
 
@@ -360,133 +360,145 @@ __device__ __forceinline__ bool is_desc(uint32_t q, uint32_t qt) {  // heap node
 __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
     const LfinArgs &A = L.args;
     const Tv16FillBucket &d = A.d;
-    const uint32_t tid = threadIdx.x, nc = A.nc;
+    const uint32_t tid = threadIdx.x;
     LfinDec D;
     LF_STAMP(0);
     if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[28] = (uint32_t)__builtin_amdgcn_s_memtime();  // the shader clock
+    constexpr uint32_t PB = NBIN / FILL_WG;  // bins per thread
+    static_assert(PB == 2 && NBIN == LNBIN, "two bins per thread");
+    uint32_t h[PB];  // the scan's window entries per bin, in flight with the prefix's loads
+#pragma unroll
+    for (uint32_t u = 0; u < PB; ++u) h[u] = A.whist[PB * tid + u];
     lfin_prefix(L, A, D);
     LF_STAMP(1);
     if (!D.regimeB || (!D.M && !D.tail_cand)) return;  // nothing to fill
+    auto give_up = [&]() {
+        if (rk == 0 && threadIdx.x == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+    };
     if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_RANKED);
     const uint32_t tb = f2u(D.t), wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
     const bool tail_in = D.tail_cand && D.tail_key >= u2f(wlo);
     const uint32_t W = D.Wtot + (tail_in ? 1u : 0u);
-    if (!D.listw || !D.lists_ok || D.N > POS_LIM || W == 0 || A.mode) {
-        if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+    // a -0.0 tail ties +0.0 sums in the reference's float compare, not in ford() order
+    if (!D.listw || !D.lists_ok || D.N > POS_LIM || W == 0 || A.mode ||
+        (tail_in && (f2u(D.tail_key) & 0x80000000u))) {
+        give_up();
         return;
     }
-    auto kbin = [&](uint32_t ok) -> uint32_t {  // 256-ulp bins below t, sum descending (ok = ford(sum))
-        const float k = u2f(ok & 0x80000000u ? ok & 0x7fffffffu : ~ok);
-        if (k >= D.t) return 0u;
-        if (!(k > 0.f)) return NBIN - 1;
-        return min((tb - 1u - f2u(k)) >> 8, NBIN - 1);
-    };
-    // ---- the window: entry -> chunk (a thread per chunk), then each
-    //      thread's entries loaded together into registers, binned there ----
-    for (uint32_t c = tid; c < nc; c += FILL_WG)
-        for (uint32_t e = L.wp[c]; e < L.wp[c + 1]; ++e) L.u.r.emap[e] = (uint16_t)c;
-    for (uint32_t i = tid; i < NBIN; i += FILL_WG) L.bin[i] = 0;
-    __syncthreads();
-    LF_STAMP(2);
-    constexpr uint32_t KW = CAND_CAP / FILL_WG;  // entries per thread: e = tid + k * FILL_WG
-    static_assert(KW * FILL_WG == CAND_CAP, "window entries per thread");
-    uint32_t ok[KW], cx[KW], ln[KW];
-    {
-        uint2 x[KW];
-        uint32_t c[KW];
-#pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) {
-            const uint32_t e = tid + k * FILL_WG;
-            c[k] = 0;
-            if (e < D.Wtot) {
-                c[k] = L.u.r.emap[e];
-                x[k] = A.lw[(size_t)c[k] * LWCAP + (e - L.wp[c[k]])];
-            }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) {
-            const uint32_t e = tid + k * FILL_WG;
-            ok[k] = 0;
-            if (e < D.Wtot) {
-                const uint32_t line = c[k] * LCHUNK + (x[k].y & 0xffffu);
-                ok[k] = ford(u2f(x[k].x));
-                cx[k] = line - (L.qp[c[k]] + (x[k].y >> 16));
-                ln[k] = line;
-            } else if (e == D.Wtot && tail_in) {  // the ragged tail: the candidate vector's last entry
-                ok[k] = ford(D.tail_key);          // (thresholdv16.cpp:229-234)
-                cx[k] = D.N - 1;
-                ln[k] = d.nb;
-            }
-            if (e < W) atomicAdd(&L.bin[kbin(ok[k])], 1u);
-        }
+    // the tail's window offset and bin, as the scan bins a sum (a tail key
+    // rounded up to t would sort above the window: the orderer takes it)
+    if (tail_in && !(D.tail_key < D.t)) {
+        give_up();
+        return;
     }
-    __syncthreads();
-    LF_STAMP(3);
-    // ---- keep the first bins holding M + 2 entries: every pop, the first
-    //      line past them and its ties (a bin never splits equal sums) ----
+    const uint32_t tw = tail_in ? tb - 1u - f2u(D.tail_key) : 0u, tbin = tail_in ? tw >> 8 : NONE;
+    // ---- bin starts; keep the first bins holding M + 2 entries: every pop,
+    //      the first line past them and its ties (a bin never splits equal sums) ----
+    const uint32_t need = D.M + 2;
     {
-        constexpr uint32_t PER = NBIN / FILL_WG;
-        static_assert(PER == 2, "two bins per thread");
-        const uint32_t b0 = L.bin[PER * tid], b1 = L.bin[PER * tid + 1], need = D.M + 2;
+        const uint32_t b0 = PB * tid, c0 = h[0] + (b0 == tbin ? 1u : 0u), c1 = h[1] + (b0 + 1 == tbin ? 1u : 0u);
         uint32_t tot;
-        const uint32_t run = blk_excl_scan<FNW_F>(b0 + b1, L.sh, &tot);
-        L.bin[PER * tid] = L.u.r.cur[PER * tid] = run;
-        L.bin[PER * tid + 1] = L.u.r.cur[PER * tid + 1] = run + b0;
-        if (run < need && run + b0 >= need) { L.cut = PER * tid + 1; L.wk = run + b0; }
-        else if (run + b0 < need && run + b0 + b1 >= need) { L.cut = PER * tid + 2; L.wk = run + b0 + b1; }
-        if (tid == 0 && tot < need) { L.cut = NBIN; L.wk = tot; }
-        if (tid == 0) { L.tail_e = NONE; L.nbl = 0; L.nlate = 0; }
+        const uint32_t run = blk_excl_scan<FNW_F>(c0 + c1, L.sh, &tot);
+        L.bin[b0] = run;
+        L.bin[b0 + 1] = run + c0;
+        if (run < need && run + c0 >= need) { L.cut = b0 + 1; L.wk = run + c0; }
+        else if (run + c0 < need && run + c0 + c1 >= need) { L.cut = b0 + 2; L.wk = run + c0 + c1; }
+        if (tid == 0) {
+            L.bin[NBIN] = tot;
+            if (tot < need) { L.cut = NBIN; L.wk = tot; }
+            L.tail_rank = NONE;
+            L.nlate = 0;
+        }
         __syncthreads();
     }
     const uint32_t cut = L.cut, Wk = L.wk;
     const uint32_t rem = d.dst_len - D.cnt;
-    if (Wk > EMAX || Wk == 0 || 16u * Wk < rem) {
-        if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+    // a kept bin with more entries than the scan could store, or too many kept
+    const bool over = (PB * tid < cut && h[0] > LBCAP) || (PB * tid + 1 < cut && h[1] > LBCAP);
+    if (__syncthreads_or((int)over) || Wk > EMAX || Wk == 0 || 16u * Wk < rem) {
+        give_up();
         return;
     }
-    LF_STAMP(4);
-    // ---- the kept lines, compacted from registers, and grouped by bin ----
-    uint32_t *const kk = L.u.r.kk, *const kc = L.u.r.kc, *const kr = L.u.r.kr, *const kl = L.u.r.kl;
+    LF_STAMP(2);
+    uint64_t *const kg = L.u.r.kg;
+    uint32_t *const kc = L.u.r.kc, *const kl = L.u.r.kl;
+    uint16_t *const emap = L.u.r.emap, *const ord = L.u.r.ord;
+    uint8_t *const tf = L.u.r.tf;
+#pragma unroll
+    for (uint32_t u = 0; u < PB; ++u) {
+        const uint32_t b = PB * tid + u;
+        if (b < cut)
+            for (uint32_t e = L.bin[b]; e < L.bin[b + 1]; ++e) emap[e] = (uint16_t)b;
+    }
+    __syncthreads();
+    // ---- the kept entries, loaded together, decoded into LDS ----
+    constexpr uint32_t KE = EMAX / FILL_WG;
+    auto is_tail = [&](uint32_t e, uint32_t b) { return b == tbin && e + 1 == L.bin[b + 1]; };  // its bin's last
     {
-        uint32_t n = 0;
+        uint2 x[KE];
 #pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) n += (tid + k * FILL_WG < W && kbin(ok[k]) < cut) ? 1u : 0u;
-        uint32_t tot;
-        uint32_t o = blk_excl_scan<FNW_F>(n, L.sh, &tot);
-#pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) {
-            const uint32_t e = tid + k * FILL_WG;
-            if (e < W) {
-                const uint32_t b = kbin(ok[k]);
-                if (b < cut) {
-                    kk[o] = ok[k];
-                    kc[o] = cx[k];
-                    kr[o] = rf_key(cx[k]);
-                    kl[o] = ln[k];
-                    L.u.r.bl2[atomicAdd(&L.u.r.cur[b], 1u)] = (uint16_t)o;
-                    if (e == D.Wtot) L.tail_e = o;
-                    ++o;
-                }
+        for (uint32_t j = 0; j < KE; ++j) {
+            const uint32_t e = tid + j * FILL_WG;
+            x[j] = make_uint2(0u, 0u);
+            if (e < Wk) {
+                const uint32_t b = emap[e];
+                if (!is_tail(e, b)) x[j] = A.went[b * LBCAP + (e - L.bin[b])];
             }
         }
-        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < KE; ++j) {
+            const uint32_t e = tid + j * FILL_WG;
+            if (e >= Wk) continue;
+            uint32_t w, cx, line;
+            if (is_tail(e, emap[e])) {  // the candidate vector's last entry (thresholdv16.cpp:229-234)
+                w = tw;
+                cx = D.N - 1;
+                line = d.nb;
+            } else {
+                const uint32_t c = x[j].y >> 19;
+                line = c * LCHUNK + ((x[j].y >> 10) & 511u);
+                w = tb - 1u - x[j].x;
+                cx = line - (L.qp[c] + (x[j].y & 1023u));
+            }
+            kg[e] = (uint64_t)w << 25 | rf_key(cx);
+            kc[e] = cx;
+            kl[e] = line;
+        }
     }
-    LF_STAMP(5);
-    // order: (key desc, right-first pre-order of the start position asc)
-    auto before = [&](uint32_t f, uint32_t e) { return kk[f] > kk[e] || (kk[f] == kk[e] && kr[f] < kr[e]); };
-    auto rank_of = [&](uint32_t e) {  // its bin's start + the bin's lines before it
-        const uint32_t b = kbin(kk[e]), hi = L.u.r.cur[b];
-        uint32_t r = L.bin[b];
-        for (uint32_t x = L.bin[b]; x < hi; ++x) r += before(L.u.r.bl2[x], e);
-        return r;
-    };
-    // ---- the tail's rank, then the pops P of tv16fill.hip ----
-    const uint32_t te = L.tail_e;
-    if (te != NONE && tid == 0) L.tail_rank = rank_of(te);
     __syncthreads();
-    const uint32_t tr = te != NONE ? L.tail_rank : NONE;
-    if (te != NONE && 16u * Wk - (16u - d.tl) < rem) {
-        if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
+    LF_STAMP(3);
+    // ---- ranks: (sum desc = window offset asc, right-first pre-order of the
+    //      start position asc) = kg asc; the bins are ordered, so an entry's
+    //      rank is its bin's start plus the bin's smaller keys.  Ties (equal
+    //      offsets) are noted for the fast path's check (3) ----
+    for (uint32_t e = tid; e < Wk; e += FILL_WG) {
+        const uint32_t b = emap[e], lo = L.bin[b], hi = L.bin[b + 1];
+        const uint64_t ge = kg[e];
+        const uint32_t we = (uint32_t)(ge >> 25);
+        uint32_t r = lo;
+        bool tie = false;
+        for (uint32_t x = lo; x < hi; ++x) {
+            const uint64_t gx = kg[x];
+            r += gx < ge;
+            tie |= (uint32_t)(gx >> 25) == we && gx != ge;
+        }
+        uint32_t f = 0;
+        if (tie) {  // rare: is a tied line's start below this one's?
+            f = LF_TIES;
+            const uint32_t qe = kc[e] + 1;
+            for (uint32_t x = lo; x < hi; ++x)
+                if (x != e && (uint32_t)(kg[x] >> 25) == we && is_desc(kc[x] + 1, qe)) f |= LF_VIOL;
+        }
+        tf[e] = (uint8_t)f;
+        ord[r] = (uint16_t)e;
+        if (is_tail(e, b)) L.tail_rank = r;
+    }
+    __syncthreads();
+    LF_STAMP(4);
+    // ---- the pops P and the bound Ph of tv16fill.hip; R = keys >= the key at rank Ph ----
+    const uint32_t tr = L.tail_rank;
+    if (tr != NONE && 16u * Wk - (16u - d.tl) < rem) {
+        give_up();
         return;
     }
     uint32_t P = (rem + 15u) / 16u;  // the first rank whose output offset reaches rem
@@ -495,97 +507,93 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
     // conservative bounds for the fast-path conditions: one more pop than P
     // (the exact orderer counts its pops in (sum desc, index asc) order)
     const uint32_t Ph = min(P + 1, Wk - 1);
-    // ---- the key at rank Ph: its bin, then the bin's keys ranked among themselves ----
-    {
-        constexpr uint32_t PER = NBIN / FILL_WG;
-#pragma unroll
-        for (uint32_t u = 0; u < PER; ++u) {
-            const uint32_t b = PER * tid + u;
-            if (b < cut && L.bin[b] <= Ph && Ph < L.u.r.cur[b]) L.kh = b;
-        }
-        __syncthreads();
-        const uint32_t bh = L.kh, lo = L.bin[bh], nb = L.u.r.cur[bh] - lo;
-        if (nb > 64) {
-            if (rk == 0 && tid == 0) g_or(&A.cc->pad[5], LF_FALLBACK);
-            return;
-        }
-        if (tid < nb) L.bl[tid] = kk[L.u.r.bl2[lo + tid]];
-        __syncthreads();
-        if (tid < nb) {
-            const uint32_t k = L.bl[tid];
-            uint32_t gt = 0, eq = 0;
-            for (uint32_t i = 0; i < nb; ++i) { gt += L.bl[i] > k; eq += L.bl[i] == k; }
-            if (gt <= Ph - lo && Ph - lo < gt + eq) L.kh = k;
-        }
-        __syncthreads();
-    }
-    LF_STAMP(6);
-    const uint32_t KH = L.kh;  // R: the kept lines with key >= KH
     const uint32_t late = D.N > Ph + 1 ? D.N - (Ph + 1) : 0u;  // start positions >= late: the last Ph + 1
-    // ---- this ranker's share: a thread per line, its rank within its bin;
-    //      tie and structure checks (tv16fill.hip (3)) ----
-    const uint32_t nr = A.rankers, per = (Wk + nr - 1) / nr;
-    const uint32_t s0 = min(Wk, rk * per), s1 = min(Wk, s0 + per);
-    uint32_t fl = 0;
-    for (uint32_t e = s0 + tid; e < s1; e += FILL_WG) {
-        const uint32_t ke = kk[e], ce = kc[e], qe = ce + 1;
-        const bool inR = ke >= KH;
-        const uint32_t b = kbin(ke), hi = L.u.r.cur[b];
-        uint32_t r = L.bin[b];
-        for (uint32_t x = L.bin[b]; x < hi; ++x) {
-            const uint32_t g = L.u.r.bl2[x];
-            r += before(g, e);
-            if (g != e && kk[g] == ke && inR) {
-                fl |= LF_TIES;
-                if (is_desc(kc[g] + 1, qe)) fl |= LF_VIOL;  // (3): a tied line starting below this one
-            }
+    // ---- this ranker's share of the pops: four lanes per line, the loads of
+    //      NRD rounds in flight (issued now, stored after the checks) ----
+    const uint32_t nr = A.rankers, per = (P + nr - 1) / nr;
+    const uint32_t s0 = min(P, rk * per), s1 = min(P, s0 + per);
+    const bool vec = aligned16(d) && (D.cnt & 3u) == 0;
+    auto offset = [&](uint32_t i) { return 16u * i - (tr < i ? 16u - d.tl : 0u); };
+    constexpr uint32_t LPR = FILL_WG / 4, NRD = 4;
+    const uint32_t q = tid & 3u;
+    float4 v0, v1, v2, v3;
+    uint32_t pos[NRD], off[NRD], len[NRD];
+#define LF_LOAD_ROUND(J0)                                                                   \
+    do {                                                                                    \
+        _Pragma("unroll") for (uint32_t u = 0; u < NRD; ++u) {                              \
+            const uint32_t i = (J0) + u * LPR + (tid >> 2);                                 \
+            len[u] = 0;                                                                     \
+            if (i < s1) {                                                                   \
+                off[u] = offset(i);                                                         \
+                if (off[u] < rem) {                                                         \
+                    len[u] = min(i == tr ? d.tl : 16u, rem - off[u]);                       \
+                    pos[u] = kl[ord[i]] * 16;                                               \
+                }                                                                           \
+            }                                                                               \
+        }                                                                                   \
+        auto ld4 = [&](uint32_t u) {                                                        \
+            return (vec && len[u] == 16 && (off[u] & 3u) == 0)                              \
+                       ? reinterpret_cast<const float4 *>(d.src + pos[u])[q]                \
+                       : make_float4(0.f, 0.f, 0.f, 0.f);                                   \
+        };                                                                                  \
+        v0 = ld4(0); v1 = ld4(1); v2 = ld4(2); v3 = ld4(3);                                 \
+    } while (0)
+    auto store1 = [&](uint32_t u, float4 x) {
+        if (!len[u]) return;
+        const uint32_t o = D.cnt + off[u] + 4 * q, bi = pos[u] + 4 * q + (uint32_t)d.idx_offset;
+        if (vec && len[u] == 16 && (off[u] & 3u) == 0) {
+            *reinterpret_cast<float4 *>(d.val + o) = x;
+            *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+        } else {
+            for (uint32_t cc = 0; cc < 4; ++cc)
+                if (4 * q + cc < len[u]) {
+                    d.val[o + cc] = d.src[(size_t)pos[u] + 4 * q + cc];
+                    d.idx[o + cc] = bi + cc;
+                }
         }
-        L.u.r.rr[e - s0] = (uint16_t)r;
-        if (inR && ce >= late && ce) {  // a late line of R: checked below by the whole workgroup
+    };
+    LF_LOAD_ROUND(s0);
+    // ---- the fast path's conditions (tv16fill.hip (3)) for R; every ranker
+    //      finds the same, ranker 0 reports ----
+    const uint32_t wh = (uint32_t)(kg[ord[Ph]] >> 25);  // R: window offsets <= wh
+    uint32_t fl = 0;
+    for (uint32_t e = tid; e < Wk; e += FILL_WG) {
+        if ((uint32_t)(kg[e] >> 25) > wh) continue;
+        fl |= tf[e];
+        const uint32_t ce = kc[e];
+        if (ce >= late && ce) {  // a late line of R
             const uint32_t i = atomicAdd(&L.nlate, 1u);
             if (i < 64) L.late[i] = ce;
         }
     }
     __syncthreads();
-    LF_STAMP(7);
-    {   // (3): no line of R at a late line's parent or sibling -- every thread
-        // takes its kept lines against every late one
+    {   // no line of R at a late line's parent or sibling
         const uint32_t nl = L.nlate;
         if (nl > 64) fl |= LF_VIOL;
         else if (nl)
             for (uint32_t f = tid; f < Wk; f += FILL_WG) {
-                if (kk[f] < KH) continue;
+                if ((uint32_t)(kg[f] >> 25) > wh) continue;
                 const uint32_t cf = kc[f];
-                for (uint32_t j = 0; j < nl; ++j) {
-                    const uint32_t ce = L.late[j];
+                for (uint32_t i = 0; i < nl; ++i) {
+                    const uint32_t ce = L.late[i];
                     if (cf == (ce - 1) / 2 || cf == ((ce - 1) ^ 1u) + 1) fl |= LF_VIOL;
                 }
             }
     }
-    LF_STAMP(8);
-    // ---- emit the share's pops: four lanes per line ----
-    const bool vec = aligned16(d) && (D.cnt & 3u) == 0;
-    auto offset = [&](uint32_t i) { return 16u * i - (tr < i ? 16u - d.tl : 0u); };
-    for (uint32_t j = s0 + (tid >> 2); j < s1; j += FILL_WG / 4) {
-        const uint32_t q = tid & 3u, i = L.u.r.rr[j - s0], off = offset(i);
-        if (i >= P || off >= rem) continue;
-        const uint32_t len = min(i == tr ? d.tl : 16u, rem - off);
-        const uint32_t pos = kl[j] * 16, o = D.cnt + off + 4 * q, bi = pos + 4 * q + (uint32_t)d.idx_offset;
-        if (vec && len == 16 && (off & 3u) == 0) {
-            *reinterpret_cast<float4 *>(d.val + o) = reinterpret_cast<const float4 *>(d.src + pos)[q];
-            *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
-        } else {
-            for (uint32_t cc = 0; cc < 4; ++cc)
-                if (4 * q + cc < len) {
-                    d.val[o + cc] = d.src[(size_t)pos + 4 * q + cc];
-                    d.idx[o + cc] = bi + cc;
-                }
-        }
+    LF_STAMP(5);
+    store1(0, v0); store1(1, v1); store1(2, v2); store1(3, v3);
+    for (uint32_t j0 = s0 + NRD * LPR; j0 < s1; j0 += NRD * LPR) {
+        LF_LOAD_ROUND(j0);
+        store1(0, v0); store1(1, v1); store1(2, v2); store1(3, v3);
     }
+#undef LF_LOAD_ROUND
     const bool ties = __syncthreads_or((int)(fl & LF_TIES));
     const bool viol = __syncthreads_or((int)(fl & LF_VIOL));
-    if (tid == 0 && (viol || ties)) g_or(&A.cc->pad[5], (ties ? LF_TIES : 0u) | (viol ? LF_VIOL : 0u));
+    if (rk == 0 && tid == 0 && (viol || ties)) g_or(&A.cc->pad[5], (ties ? LF_TIES : 0u) | (viol ? LF_VIOL : 0u));
     if (STG_FILL_STAMPS && rk == STG_FILL_STAMPS_RK && tid == 0) { A.dbg[44] = Wk; A.dbg[45] = P; A.dbg[46] = s1 - s0; A.dbg[47] = fl; }
+    LF_STAMP(6);
+    LF_STAMP(7);
+    LF_STAMP(8);
     LF_STAMP(9);
     if (STG_FILL_STAMPS && rk == 0 && tid == 0) A.dbg[29] = (uint32_t)__builtin_amdgcn_s_memtime();
 }

@@ -50,6 +50,9 @@ using namespace tv16;
 #define STG_LSCAN_DIAG 0
 #endif
 
+static_assert(LCHUNK <= 512 && LMAXC <= 4096 && LQCAP < 1024, "binned entry packing: chunk:12 | line:9 | qb:10");
+static_assert(LNBIN << 8 == TV16_WIN, "bins of 256 ulps cover the window");
+
 struct LLds {
     float4 qv[2][LQCAP][4];  // their data (a float4 per lane of the line's quad)
     uint32_t ql[2][LQCAP];  // qualifying lines of the chunk in the slot (unordered)
@@ -58,11 +61,21 @@ struct LLds {
 };
 
 // A slot's lists, ordered, to global memory: by the last wave done with the
-// chunk.  Ranks by counting (a few dozen entries per chunk at k = 1 %).
-__device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t sl, uint32_t c, uint32_t j) {
+// chunk.  Ranks by counting (a few dozen entries per chunk at k = 1 %).  Its
+// window lines also go to their bins (ws.h LNBIN): the bin's count is taken
+// first, so the atomic's round trip overlaps the list writes.
+__device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t sl, uint32_t c, uint32_t j,
+                                         uint32_t tb) {
     const uint32_t lane = flane();
     const uint32_t qn = uni(lds_ld(&L.qn[sl])), wn = uni(lds_ld(&L.wn[sl]));
     const uint32_t ql = std::min(qn, LQCAP), wlc = std::min(wn, LWCAP);
+    static_assert(LWCAP <= 64, "one window entry per lane");
+    const uint64_t we = lane < wlc ? L.wl[sl][lane] : ~0ull;
+    uint32_t wbin = 0, wslot = LBCAP;
+    if (lane < wlc) {
+        wbin = (tb - 1u - (uint32_t)(we >> 32)) >> 8;  // < LNBIN: the sum is in [t - 2^18 ulps, t)
+        wslot = g_add(&A.whist[wbin], 1u);
+    }
     uint32_t *lq = A.lq + (size_t)c * LQCAP;
     uint2 *lw = A.lw + (size_t)c * LWCAP;
     float4 *lv = A.lv + (size_t)c * LQCAP * 4;
@@ -79,13 +92,14 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
         }
     }
     if (wlc) {  // at most one entry per lane
-        static_assert(LWCAP <= 64, "one window entry per lane");
-        const uint64_t e = lane < wlc ? L.wl[sl][lane] : ~0ull;
-        const uint32_t li = (uint32_t)e;
+        const uint32_t li = (uint32_t)we;
         uint32_t r = 0, qb = 0;
         for (uint32_t x = 0; x < wlc; ++x) r += (uint32_t)L.wl[sl][x] < li;
         for (uint32_t x = 0; x < ql; ++x) qb += L.ql[sl][x] < li;
-        if (lane < wlc) lw[r] = make_uint2((uint32_t)(e >> 32), li | qb << 16);
+        if (lane < wlc) {
+            lw[r] = make_uint2((uint32_t)(we >> 32), li | qb << 16);
+            if (wslot < LBCAP) A.went[wbin * LBCAP + wslot] = make_uint2((uint32_t)(we >> 32), c << 19 | li << 10 | qb);
+        }
     }
     if (lane == 0) A.ldesc[c] = make_uint2(qn, wn);
     lds_drain();
@@ -216,7 +230,7 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
                 lds_drain();
                 if (lane == 0) lds_st(&L.fin[sl], j + 1);
             } else {
-                finalize(L, A, sl, c, j);
+                finalize(L, A, sl, c, j, tb);
             }
         }
     }

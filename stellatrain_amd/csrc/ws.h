@@ -86,6 +86,12 @@ constexpr uint32_t LCHUNK = 512;  // lines (16 floats) per chunk = 32 KiB: one p
 constexpr uint32_t LQCAP = 64;    // qualifying lines listed per chunk (~5 at k = 1 %; more: the finish re-reads it)
 constexpr uint32_t LWCAP = 32;    // window lines listed per chunk (~2; more: likewise)
 constexpr uint32_t LMAXC = 4096;  // chunks of a bucket the one-bucket path takes (128 MiB)
+// ... and its window entries binned by the scan: bin b = (bits(t) - 1 - bits(sum)) >> 8
+// (256 ulps, 1024 bins over the window), LBCAP entries per bin {sum bits,
+// chunk << 19 | line within the chunk << 10 | qualifying lines before it};
+// the counts are zeroed by the finish's last workgroup after use
+constexpr uint32_t LNBIN = 1024;
+constexpr uint32_t LBCAP = 32;
 
 struct DevWS {
     FillCtl *ctl;
@@ -105,6 +111,8 @@ struct DevWS {
     uint32_t *lq;        // ... the chunk's qualifying lines in order (LQCAP per chunk, line within the chunk)
     uint2 *lw;           // ... its window lines in order: {sum bits, line within the chunk | qualifying before << 16}
     float4 *lv;          // ... the qualifying lines' data (LQCAP x 4 float4 per chunk)
+    uint32_t *whist;     // ... window entries per bin (LNBIN, zero between calls)
+    uint2 *went;         // ... the entries by bin (LNBIN x LBCAP)
 };
 
 // ---- launchers (implemented in the .hip files) ----
@@ -168,6 +176,8 @@ struct Tv16FillArgs {
     const uint32_t *lq;
     const uint2 *lw;
     const float4 *lv;
+    uint32_t *whist;       // the scan's binned window (counts zeroed by the last workgroup)
+    const uint2 *went;
     uint32_t rankers;      // workgroups that order the regime-B fill in parallel (0: the orderer alone)
     KeyState *state;
     const CallParams *cp;  // {t, inc} as the scan read them
@@ -187,6 +197,8 @@ struct LScanArgs {
     uint32_t *lq;
     uint2 *lw;
     float4 *lv;
+    uint32_t *whist;       // window entries per bin (zero at the start of the call)
+    uint2 *went;           // ... and the entries, LBCAP per bin
     uint32_t *zero_next;   // the next call's counter block (CallCtl), zeroed here
 };
 hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s);

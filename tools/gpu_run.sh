@@ -78,6 +78,9 @@ for s in "$@"; do
             done ;;
         lone_bench) step lone_bench 200 ./tools/lone_bench 16 96 ;;
         prof_lone_bench) step prof_lone_bench 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lone_bench" -o run -- ./tools/lone_bench 16 96 ;;
+        prof_lone)  # kernel durations of the single-caller lone bench (production library)
+            step prof_lone 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_lone" -o run -- ./tools/lone_bench 0 96
+            python3 tools/ktrace.py gpurun_out/prof_lone 12 > gpurun_out/prof_lone.txt 2>&1 ;;
         lfin_probe) step lfin_probe 200 python tools/lfin_probe.py ;;
         prof_lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step prof_lfin_stamps 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lfin_stamps" -o run -- python3 tools/lfin_probe.py ;;
         lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step lfin_stamps 200 python tools/lfin_probe.py ;;
