@@ -149,11 +149,20 @@ int stg_codec_check(stg_codec_t h);
  * unique1d :14-24).  world > 1: output index-ascending, d_dense (n floats,
  * zero) and d_mark (n bytes, zero, 16-byte aligned) are caller scratch and
  * are left zero.  world == 1: no dense scratch; the winners in stream order.
- * Indices >= n are dropped.  *d_out_count (device) gets the union size.
- * Internal scratch is kept per (device, stream). */
+ * Indices >= n are dropped.  *d_out_count (device) gets the union size
+ * (0xffffffff after a device failure).  Internal scratch is kept per (device,
+ * stream) for reuse: 4 B per element of the largest n seen (8 B when world >
+ * 1) plus 12 B per 4,096-pair tile -- about 64 MiB for n = 16 Mi at world 1,
+ * 128 MiB at world > 1 -- until stg_scatter_merge_release. */
 int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t per_rank, int world, size_t n,
                              float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
                              uint32_t *d_out_count, void *stream);
+/* The MERGE decompress scratch of (current device, stream): syncs the stream
+ * and returns STG_ERR_DEVICE if a call on it hit a device failure (sticky). */
+int stg_scatter_merge_check(void *stream);
+/* Frees the MERGE decompress scratch of (current device, stream) after its
+ * work is done (call it before destroying a stream that merged). */
+int stg_scatter_merge_release(void *stream);
 
 /* Error feedback of the MERGE compress (engine/modules/compress.cpp:172-186):
  * after compressing d_grad into numel (idx, val) slots, zero d_grad at every

@@ -54,6 +54,8 @@ _SIGS = {
     "stg_codec_get_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "stg_scatter_merge_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_size_t, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "stg_scatter_merge_check": (C.c_int, [C.c_void_p]),
+    "stg_scatter_merge_release": (C.c_int, [C.c_void_p]),
     "stg_error_feedback_device": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p]),
     "stg_sgd_create": (C.c_int, [C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int,
                                  C.POINTER(C.c_void_p)]),

@@ -312,6 +312,7 @@ struct Win1Args {
     uint32_t *out_idx;
     float *out_val;
     uint32_t *out_count;
+    uint32_t *fail;     // sticky failure word: a tile whose look-back gave up
 };
 
 __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
@@ -361,16 +362,27 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     }
     __syncthreads();
     const uint64_t P = s_P;
+    const bool bad = s_bad != 0;
+    // a tile that gave up has no valid offset: it writes nothing, marks the
+    // scratch's sticky failure word (stg_scatter_merge_check) and, as the last
+    // tile, poisons the count; the last tile also poisons it for any earlier
+    // tile that gave up first
+    if (bad && tid == 0) g_or(a.fail, FAIL_SPIN_TIMEOUT);
 #pragma unroll
     for (uint32_t b = 0; b < WPER; ++b) {
         if (keep >> b & 1u) {
-            a.out_idx[P + r] = j[b];
-            a.out_val[P + r] = (0.0f + v[b]) / 1.0f;
+            if (!bad) {
+                a.out_idx[P + r] = j[b];
+                a.out_val[P + r] = (0.0f + v[b]) / 1.0f;
+            }
             a.win[j[b]] = 0;  // scratch back to zero for the next call
             ++r;
         }
     }
-    if (tid == 0 && tile == a.ntiles - 1) *a.out_count = s_bad ? 0xffffffffu : (uint32_t)(P + tc);
+    if (tid == 0 && tile == a.ntiles - 1) {
+        __builtin_amdgcn_s_waitcnt(0);
+        *a.out_count = (bad || ld_sc1(a.fail)) ? 0xffffffffu : (uint32_t)(P + tc);
+    }
 }
 
 __global__ void __launch_bounds__(STG_WG) sgd_apply(SgdLaunch a) {
@@ -609,7 +621,8 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
         win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win);
         const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
         if (w1.desc) {  // count and emit in one launch (tagged tile counts, look-back)
-            Win1Args a{idx, val, per_rank, n, nt, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count};
+            Win1Args a{idx, val, per_rank, n, nt, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count,
+                       w1.fail};
             win_emit1t<<<nt, STG_WG, 0, s>>>(a);
             if (w1.grid_out) *w1.grid_out = nt;
             return hipGetLastError();

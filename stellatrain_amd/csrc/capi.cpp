@@ -576,6 +576,15 @@ struct MergeScratch {
     uint64_t *desc = nullptr, *ticket = nullptr;
     uint64_t tbase = 0;
     uint32_t tag = 0;
+    uint32_t *fail = nullptr;  // sticky device failure word (a look-back that gave up)
+    ~MergeScratch() {
+        (void)hipSetDevice(device);
+        (void)hipFree(tiles);
+        (void)hipFree(win);
+        (void)hipFree(desc);
+        (void)hipFree(ticket);
+        (void)hipFree(fail);
+    }
 };
 std::mutex g_merge_mu;
 std::map<std::pair<int, hipStream_t>, std::unique_ptr<MergeScratch>> g_merge;
@@ -606,6 +615,10 @@ int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_ra
         HIP_TRY(hipMalloc(&m->ticket, sizeof(uint64_t)));
         HIP_TRY(hipMemsetAsync(m->ticket, 0, sizeof(uint64_t), s));
         m->tbase = 0;
+    }
+    if (!m->fail) {
+        HIP_TRY(hipMalloc(&m->fail, sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(m->fail, 0, sizeof(uint32_t), s));
     }
     const size_t words = std::max<size_t>(world > 1 ? 2 * n : n, 1);  // world > 1: two election halves
     if (words > m->cap_win) {
@@ -916,10 +929,53 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
     if (rc) return rc;
     if (++ms->tag == 0) ms->tag = 1;
     uint32_t grid = 0;
-    const stg::Win1Desc w1{ms->desc, ms->ticket, ms->tbase, ms->tag, &grid};
+    const stg::Win1Desc w1{ms->desc, ms->ticket, ms->tbase, ms->tag, &grid, ms->fail};
     HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, n, d_dense, d_mark, d_out_idx, d_out_val,
                                       d_out_count, ms->tiles, ms->win, ncu, s, w1));
     ms->tbase += grid;
+    return STG_OK;
+}
+
+int stg_scatter_merge_check(void *stream) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    MergeScratch *ms = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_merge_mu);
+        auto it = g_merge.find({dev, s});
+        if (it == g_merge.end()) return STG_OK;  // no merge on this stream yet
+        ms = it->second.get();
+    }
+    std::lock_guard<std::mutex> g(ms->mu);
+    HIP_TRY(hipStreamSynchronize(s));
+    uint32_t f = 0;
+    if (ms->fail) HIP_TRY(hipMemcpy(&f, ms->fail, sizeof f, hipMemcpyDeviceToHost));
+    if (f) {
+        char b[96];
+        snprintf(b, sizeof b, "MERGE decompress device failure flags 0x%x (a look-back gave up)", f);
+        return fail(STG_ERR_DEVICE, b);
+    }
+    return STG_OK;
+}
+
+int stg_scatter_merge_release(void *stream) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::unique_ptr<MergeScratch> ms;
+    {
+        std::lock_guard<std::mutex> g(g_merge_mu);
+        auto it = g_merge.find({dev, s});
+        if (it == g_merge.end()) return STG_OK;
+        ms = std::move(it->second);
+        g_merge.erase(it);
+    }
+    {
+        std::lock_guard<std::mutex> g(ms->mu);  // no call of another thread still inside
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    ms.reset();
     return STG_OK;
 }
 

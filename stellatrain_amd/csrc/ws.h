@@ -256,6 +256,7 @@ struct Win1Desc {
     uint64_t base;        // its value when the call starts
     uint32_t tag;         // call tag >= 1
     uint32_t *grid_out;   // receives the tiles launched (the ticket advances by it)
+    uint32_t *fail;       // sticky failure word of the scratch (a look-back that gave up)
 };
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,

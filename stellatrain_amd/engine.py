@@ -156,6 +156,23 @@ def scatter_merge(idx, val, per_rank: int, world: int, n: int, dense=None, mark=
     return out_idx, out_val, count
 
 
+def scatter_merge_check(device=None) -> None:
+    """Raises CodecError when a MERGE decompress on the current stream of
+    ``device`` hit a device failure (a look-back that gave up; the count of
+    that call reads 0xffffffff).  Syncs the stream."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
+    check(lib().stg_scatter_merge_check(C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+
+
+def scatter_merge_release(device=None) -> None:
+    """Frees the MERGE decompress scratch kept for the current stream of
+    ``device`` (call before dropping a stream that merged)."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
+    check(lib().stg_scatter_merge_release(C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+
+
 def gather_slice(n: int, local_rank: int, num_gpus: int):
     """Local rank's slice [n*r/N, n*(r+1)/N) of the gather-add (cpu_gather.cpp:59-61)."""
     a, b = C.c_uint64(), C.c_uint64()

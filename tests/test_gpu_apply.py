@@ -56,6 +56,7 @@ def _rank_streams(n, per_rank, world, seed, overlap):
 def test_scatter_merge_parity(gpu, oracle, n, per_rank, world, overlap):
     import torch
     from stellatrain_amd import scatter_merge
+    from stellatrain_amd.engine import scatter_merge_check
     idx, val = _rank_streams(n, per_rank, world, 5, overlap)
     oi, ov = oracle.merge_decompress(idx, val, per_rank, world, n)
     di = torch.from_numpy(idx.view(np.int32)).to(gpu)
@@ -72,6 +73,30 @@ def test_scatter_merge_parity(gpu, oracle, n, per_rank, world, overlap):
     # scratch is handed back zeroed (the next bucket reuses it)
     assert int(torch.count_nonzero(dense).item()) == 0
     assert int(torch.count_nonzero(mark).item()) == 0
+    scatter_merge_check()  # no device failure on this stream's scratch
+
+
+def test_scatter_merge_release_and_reuse(gpu, oracle):
+    """The per-(device, stream) MERGE scratch can be released and is rebuilt
+    by the next call on that stream (world 1: the one-launch look-back path)."""
+    import torch
+    from stellatrain_amd import scatter_merge
+    from stellatrain_amd.engine import scatter_merge_check, scatter_merge_release
+    n, per_rank = 100013, 5000
+    idx, val = _rank_streams(n, per_rank, 1, 7, 0.3)
+    oi, ov = oracle.merge_decompress(idx, val, per_rank, 1, n)
+    di = torch.from_numpy(idx.view(np.int32)).to(gpu)
+    dv = torch.from_numpy(val).to(gpu)
+    for _ in range(2):
+        out_i, out_v, cnt = scatter_merge(di, dv, per_rank, 1, n)
+        m = int(cnt.item())
+        assert m == oi.size
+        gi, gv = _sorted_pairs(out_i[:m].cpu().numpy(), out_v[:m].cpu().numpy())
+        ei, ev = _sorted_pairs(oi, ov)
+        assert np.array_equal(gi, ei) and np.array_equal(gv.view(np.uint32), ev.view(np.uint32))
+        scatter_merge_check()
+        scatter_merge_release()
+    scatter_merge_release()  # nothing left: a no-op
 
 
 SGD_CASES = [

@@ -49,6 +49,9 @@ for s in "$@"; do
         prof_single) step prof_single 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_single" -o run \
                 -- python3 tools/bench_configs.py --only single ;;
         c2) step c2 300 python tools/bench_configs.py --only c2 ;;
+        tests_topk) step tests_topk 400 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_api.py -k "topk or c2" -v -m gpu --timeout 120 --timeout-method thread ;;
+        prof_c2) step prof_c2 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c2" -o run -- python3 tools/bench_configs.py --only c2
+            python3 tools/ktrace.py gpurun_out/prof_c2 > gpurun_out/prof_c2.txt 2>&1 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
         c5) step c5 300 python tools/bench_configs.py --only c5 ;;
