@@ -540,6 +540,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         if ((rc = ws->ensure(1, 2 * (size_t)stg::TV_MAXG, 1))) return rc;
         if (ws->tv_desc != ws->d.tile_cnt || ws->tv_desc_cap != ws->cap_tiles) {  // fresh memory: no stale tags
             HIP_TRY(hipMemsetAsync(ws->d.tile_cnt, 0, ws->cap_tiles * sizeof(uint32_t), s));
+            HIP_TRY(hipMemsetAsync(ws->d.tile_aux, 0, ws->cap_tiles * sizeof(uint32_t), s));
             ws->tv_desc = ws->d.tile_cnt;
             ws->tv_desc_cap = ws->cap_tiles;
         }

@@ -49,7 +49,8 @@ __global__ void tv_init_state(KeyState *st, const RSel *rs) {
 }
 
 // Range of workgroup w in float4 units; the ragged n % 4 tail belongs to the
-// last range.
+// last range.  (Ranges tapered over the tickets, so that later tickets get
+// less, measured 3-7 % slower at C3.)
 struct TvRange {
     uint64_t lo, len;
 };
@@ -70,7 +71,7 @@ struct TvArgs {
     uint32_t *count_out;
     KeyState *state;
     uint64_t *desc;      // per range: {call tag:32 | qualifier count:32}
-    uint32_t *rmax;      // per range: max |x| bits (stored before the range's desc)
+    uint64_t *rmax;      // per range: {call tag:32 | max |x| bits:32}
     uint32_t tag;        // this call's tag, >= 1
     uint64_t *ticket;    // ranges taken: monotonic over the workspace's calls (zero at creation)
     uint64_t base;       // its value when this call starts (G per earlier call)
@@ -85,7 +86,7 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     __shared__ uint32_t s_pos[LCAP];
     __shared__ float s_val[LCAP];
     __shared__ uint32_t s_n, s_r, s_cnt[TNW], s_max[TNW];
-    __shared__ uint64_t s_P;
+    __shared__ uint64_t s_P, s_psum[TNW];
     __shared__ uint32_t sh[TNW + 1];
     const uint32_t G = gridDim.x, tid = threadIdx.x;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -163,47 +164,35 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     const uint32_t listed = s_n;
     uint32_t c = 0;
     for (uint32_t i = 0; i < TNW; ++i) c += s_cnt[i];
-    if (tid == 0) {  // publish: the maximum, then the tagged count
+    if (tid == 0) {  // publish: the tagged maximum and the tagged count (no order between them)
         uint32_t m = 0;
         for (uint32_t i = 0; i < TNW; ++i) m = max(m, s_max[i]);
-        st_sc1(&a.rmax[r], m);
-        __builtin_amdgcn_s_waitcnt(0);
+        st_sc1(&a.rmax[r], ((uint64_t)a.tag << 32) | m);
         st_sc1(&a.desc[r], ((uint64_t)a.tag << 32) | c);
     }
     // look-back: the counts of ranges 0 .. r-1 (taken earlier, so held by
-    // running or finished workgroups), 64 per round trip by wave 0
-    if (wave == 0) {
-        uint64_t P = 0;
-        for (uint32_t i0 = 0; i0 < r; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            uint64_t d = i < r ? ld_sc1(&a.desc[i]) : 0ull;
-            bool pend = i < r && (uint32_t)(d >> 32) != a.tag;
-            // Stale ones: only the latest pending range (the likeliest to
-            // publish last) is polled, from one lane; then
-            // the rest are re-read once -- every lane of every waiting
-            // workgroup polling would flood the fabric the streaming loads use.
-            for (uint32_t spins = 0;; ++spins) {
-                const uint64_t pm = __ballot(pend);
-                if (!pm) break;
-                const uint32_t hl = 63u - (uint32_t)__clzll((long long)pm);
-                __builtin_amdgcn_s_sleep(8);
-                if (lane == hl) {
-                    d = ld_sc1(&a.desc[i]);
-                    pend = (uint32_t)(d >> 32) != a.tag;
-                }
-                if (!__ballot(lane == hl && pend) && pend) {
-                    d = ld_sc1(&a.desc[i]);
-                    pend = (uint32_t)(d >> 32) != a.tag;
-                }
-                if (spins > (1u << 20)) {  // ~0.5 s: give up; the count is poisoned below
-                    if (lane == 0) g_or(a.fail, FAIL_SPIN_TIMEOUT);
-                    break;
-                }
-            }
-            P += (uint32_t)d;
+    // running or finished workgroups), one per thread in one round trip;
+    // stale ones are polled by their lane with s_sleep (a few lanes at most:
+    // the ranges finish streaming together)
+    uint64_t Pl = 0;
+    bool gave_up = false;
+    if (tid < r) {
+        uint64_t d = ld_sc1(&a.desc[tid]);
+        for (uint32_t spins = 0; (uint32_t)(d >> 32) != a.tag; ++spins) {
+            __builtin_amdgcn_s_sleep(8);
+            d = ld_sc1(&a.desc[tid]);
+            if (spins > (1u << 20)) { gave_up = true; break; }  // ~0.5 s: the count is poisoned below
         }
-        P = wave_sum64(P);
-        if (lane == 0) s_P = P;
+        Pl = (uint32_t)d;
+    }
+    if (gave_up) g_or(a.fail, FAIL_SPIN_TIMEOUT);
+    Pl = wave_sum64(Pl);
+    if (lane == 0) s_psum[wave] = Pl;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t t2 = 0;
+        for (uint32_t i = 0; i < TNW; ++i) t2 += s_psum[i];
+        s_P = t2;
     }
     __syncthreads();
     const uint64_t P = s_P;
@@ -259,7 +248,15 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     // range stored its maximum before its count: fold them
     if (r != G - 1) return;
     uint32_t gm = 0;
-    for (uint32_t i = tid; i < G; i += TWG) gm = max(gm, ld_sc1(&a.rmax[i]));
+    for (uint32_t i = tid; i < G; i += TWG) {  // every range's tagged maximum
+        uint64_t x = ld_sc1(&a.rmax[i]);
+        for (uint32_t spins = 0; (uint32_t)(x >> 32) != a.tag; ++spins) {
+            __builtin_amdgcn_s_sleep(8);
+            x = ld_sc1(&a.rmax[i]);
+            if (spins > (1u << 20)) { g_or(a.fail, FAIL_SPIN_TIMEOUT); break; }
+        }
+        gm = max(gm, (uint32_t)x);
+    }
     const uint64_t cntall = P + c;
     gm = wave_max(gm);
     if (lane == 0) s_max[wave] = gm;
@@ -302,7 +299,7 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     f.count_out = a.count_out;
     f.state = a.state;
     f.desc = reinterpret_cast<uint64_t *>(ws.tile_cnt);
-    f.rmax = ws.tile_aux;
+    f.rmax = reinterpret_cast<uint64_t *>(ws.tile_aux);
     f.tag = a.tag;
     f.fail = ws.fail;
     f.ticket = ws.tv_ticket;
