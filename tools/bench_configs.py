@@ -106,8 +106,12 @@ def time_device(torch, comp, method, mib, ratio, calls, warmup, keys):
     comp.set_timing(False)
     comp.check_device()
     us = ms * 1e3 / calls
-    alg = 4.0 * n + 8.0 * k
+    # the bug-compatible "topk" reads only the first n/4 floats (memcpy of n
+    # bytes, topk.cpp:31): its roofline is priced on the bytes it moves
+    read = 4.0 * ((n + 3) // 4) if method == "topk" else 4.0 * n
+    alg = read + 8.0 * k
     return {"config": f"{method} {mib} MiB k={k}", "n": n, "k": k, "us_per_call": round(us, 2),
+            "alg_bytes": alg, "bytes_read_note": "4 ceil(n/4) + 8k (n/4 floats read)" if method == "topk" else "4n + 8k",
             "GBps_dense_in": round(4.0 * n / us / 1e3, 1),
             "alg_GBps": round(alg / us / 1e3, 1), "frac_hbm_peak": round(alg / us / 1e3 / PEAK, 4),
             "kernel_us": {"main": round(k0 * 1e3 / max(launches, 1), 2), "second": round(k1 * 1e3 / max(launches, 1), 2),
