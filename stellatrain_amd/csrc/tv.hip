@@ -76,7 +76,22 @@ struct TvArgs {
     uint64_t *ticket;    // ranges taken: monotonic over the workspace's calls (zero at creation)
     uint64_t base;       // its value when this call starts (G per earlier call)
     uint32_t *fail;      // the workspace's sticky failure word
+    uint32_t *dbg;       // diagnostics (STG_TV_STAMPS builds): phase stamps at words 40..49
 };
+
+#ifndef STG_TV_STAMPS
+#define STG_TV_STAMPS 0
+#endif
+// s_memrealtime (100 MHz) phase stamps: the maximum over the ranges by
+// atomicMax, or one range's by a plain store
+#define TV_STAMP_MAX(w)                                                                              \
+    do {                                                                                             \
+        if (STG_TV_STAMPS && threadIdx.x == 0) atomicMax(&a.dbg[w], (uint32_t)__builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#define TV_STAMP_IF(cond, w)                                                                         \
+    do {                                                                                             \
+        if (STG_TV_STAMPS && threadIdx.x == 0 && (cond)) a.dbg[w] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 // One launch: the workgroup with ticket r streams range r, publishes its count,
 // sums the counts of the earlier ranges (look-back) and writes the range's
@@ -90,6 +105,8 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     __shared__ uint32_t sh[TNW + 1];
     const uint32_t G = gridDim.x, tid = threadIdx.x;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    uint32_t t_start = 0;
+    if (STG_TV_STAMPS && tid == 0) t_start = (uint32_t)__builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
         s_n = 0;
         s_r = (uint32_t)(g_add(a.ticket, 1ull) - a.base);
@@ -99,6 +116,13 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     const float t = a.state->t;
     __syncthreads();
     const uint32_t r = s_r;  // ranges in ticket order
+    if (STG_TV_STAMPS && tid == 0) {
+        if (r == 0) a.dbg[40] = t_start;
+        atomicMax(&a.dbg[41], t_start);
+    }
+    TV_STAMP_MAX(42);  // ticket in
+    uint32_t s_tkt_time = 0;
+    if (STG_TV_STAMPS && tid == 0) s_tkt_time = (uint32_t)__builtin_amdgcn_s_memrealtime();
     const uint64_t n = a.n, n4 = n / 4;
     const TvRange R = tv_range(n4, G, r);
     // the range as a bounded buffer: lanes past it read zeros (launch_tv keeps
@@ -120,8 +144,9 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     for (uint32_t m0 = 0; m0 < mine; m0 += SCAN_D) {
 #pragma unroll
         for (uint32_t u = 0; u < SCAN_D; ++u) {
+            // consume the slot before loading into it (loading first made the
+            // compiler move registers at the back-edge behind a wait for every load)
             const float4 x = v[u];
-            v[u] = load(m0 + u + SCAN_D);
             const uint32_t f = ((m0 + u) * TNW + wave) * 64 + lane;  // float4 within the range
             const bool in = f < R.len;
             const float a0 = fabsf(x.x), a1 = fabsf(x.y), a2 = fabsf(x.z), a3 = fabsf(x.w);
@@ -143,6 +168,7 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
                     }
                 }
             }
+            v[u] = load(m0 + u + SCAN_D);
         }
     }
     // the ragged tail (n % 4 elements) closes the last range
@@ -161,6 +187,16 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     mx = wave_max(mx);
     if (lane == 0) { s_cnt[wave] = cnt; s_max[wave] = mx; }
     __syncthreads();
+    TV_STAMP_MAX(44);  // streaming done
+    if (STG_TV_STAMPS && tid == 0 && a.cap >= 4 * G) {  // per range, at the end of idx: block, start, ticket in, stream end
+        uint32_t *o = a.idx + a.cap - 4 * G + 4 * r;
+        o[0] = blockIdx.x;
+        o[1] = t_start;
+        o[2] = s_tkt_time;
+        o[3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
+    TV_STAMP_IF(r == 0, 43);
+    TV_STAMP_IF(r == G - 1, 47);
     const uint32_t listed = s_n;
     uint32_t c = 0;
     for (uint32_t i = 0; i < TNW; ++i) c += s_cnt[i];
@@ -196,8 +232,11 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     }
     __syncthreads();
     const uint64_t P = s_P;
-    if (P < a.cap && c) {
-        const uint32_t m = (uint32_t)std::min<uint64_t>(c, a.cap - P);
+    const uint32_t cap_e = STG_TV_STAMPS && a.cap >= 4 * G ? a.cap - 4 * G : a.cap;  // stamps build: keep the tail
+    TV_STAMP_MAX(45);  // look-back done
+    TV_STAMP_IF(r == G - 1, 48);
+    if (P < cap_e && c) {
+        const uint32_t m = (uint32_t)std::min<uint64_t>(c, cap_e - P);
         if (listed <= LCAP) {
             // position order: rank = listed entries with a smaller position
             for (uint32_t e = tid; e < listed; e += TWG) {
@@ -244,6 +283,7 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
             }
         }
     }
+    TV_STAMP_MAX(49);  // emission issued
     // the last range has seen every range's count (the look-back), and each
     // range stored its maximum before its count: fold them
     if (r != G - 1) return;
@@ -273,6 +313,7 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
         *a.count_out = (uint32_t)std::min<uint64_t>(cntall, a.cap);
         if (ld_sc1(a.fail)) *a.count_out = POISON_COUNT;  // a bounded wait gave up: untrusted output
     }
+    TV_STAMP_IF(true, 46);  // the fold written
 }
 
 }  // namespace
@@ -302,6 +343,7 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     f.rmax = reinterpret_cast<uint64_t *>(ws.tile_aux);
     f.tag = a.tag;
     f.fail = ws.fail;
+    f.dbg = ws.misc;
     f.ticket = ws.tv_ticket;
     f.base = a.ticket_base;
     if (a.grid_out) *a.grid_out = G;

@@ -53,6 +53,14 @@ for s in "$@"; do
         prof_c2) step prof_c2 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c2" -o run -- python3 tools/bench_configs.py --only c2
             python3 tools/ktrace.py gpurun_out/prof_c2 > gpurun_out/prof_c2.txt 2>&1 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
+        tvvar)  # threshold-v variants built by tools/tv_variants.sh: C3 device timing each
+            for L in stellatrain_amd/libstg_codec_tv*.so; do
+                v=$(basename $L .so); v=${v#libstg_codec_}
+                STG_CODEC_LIB=$R/$L step c3_$v 150 python tools/bench_configs.py --only c3dev --calls 64
+                [ -n "${TV_TESTS:-}" ] && STG_CODEC_LIB=$R/$L step tests_tv_$v 300 python -u -m pytest tests/test_gpu_codecs.py -k "thresholdv_parity" -x -q -m gpu --timeout 120 --timeout-method thread
+            done ;;
+        tv_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_tvst.so step tv_stamps 150 python tools/tv_stamps.py ;;
+        tests_tv) step tests_tv 400 python -u -m pytest tests -k "thresholdv and not thresholdv16 or c3 or tv_" -v -m gpu --timeout 120 --timeout-method thread ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
         c5) step c5 300 python tools/bench_configs.py --only c5 ;;
         apply) step apply 300 python tools/bench_configs.py --only c5,apply ;;
