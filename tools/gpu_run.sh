@@ -49,6 +49,16 @@ for s in "$@"; do
         prof_single) step prof_single 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_single" -o run \
                 -- python3 tools/bench_configs.py --only single ;;
         c2) step c2 300 python tools/bench_configs.py --only c2 ;;
+        prof_topk) step prof_topk 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_topk" -o run -- python3 tools/bench_configs.py --only topk --cpu-seconds 0
+            python3 tools/ktrace.py gpurun_out/prof_topk > gpurun_out/prof_topk.txt 2>&1 ;;
+        c2ab)  # shipped-mode top-k: the ordered six-launch path (STG_TOPK_BK=0) against the unordered three
+            STG_TOPK_BK=0 step c2_ordered 150 python tools/bench_configs.py --only topk --cpu-seconds 0
+            step c2_bk 150 python tools/bench_configs.py --only topk --cpu-seconds 0
+            for L in stellatrain_amd/libstg_codec_bk*.so; do
+                [ -e "$L" ] || continue
+                v=$(basename $L .so); v=${v#libstg_codec_}
+                STG_CODEC_LIB=$R/$L step c2_$v 150 python tools/bench_configs.py --only topk --cpu-seconds 0
+            done ;;
         tests_topk) step tests_topk 400 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_api.py -k "topk or c2" -v -m gpu --timeout 120 --timeout-method thread ;;
         prof_c2) step prof_c2 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c2" -o run -- python3 tools/bench_configs.py --only c2
             python3 tools/ktrace.py gpurun_out/prof_c2 > gpurun_out/prof_c2.txt 2>&1 ;;
