@@ -181,6 +181,15 @@ int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, u
                                 const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
                                 const uint32_t *d_grad_len, void *stream);
 int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_t len, void *stream);
+/* ModuleCpuOptimize::run (engine/modules/cpu_optimize.cpp:26-100): the MERGE
+ * decompress of the received stream (as stg_scatter_merge_device: d_out_idx /
+ * d_out_val / d_out_count get the merged stream, param_len is n) followed by
+ * SparseOptimizer::optimize_raw of `o` on it (sgd.cpp:34-263), in one call,
+ * stream-ordered, the step's length read from d_out_count on the device. */
+int stg_merge_optimize_sgd_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len,
+                                  const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
+                                  float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
+                                  uint32_t *d_out_count, void *stream);
 
 /* Sparse Adam (optim/adam.cpp:19-86; options Adam::configure adam.cpp:90-122,
  * defaults adam.h:21-23, lr sparse_optimizer.h:30).  optimize_raw() keeps per

@@ -1000,11 +1000,10 @@ int stg_sgd_destroy(stg_sgd_t o) {
     return STG_OK;
 }
 
-int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len, const float *d_grad,
-                                const uint32_t *d_idx, uint32_t grad_len, const uint32_t *d_grad_len, void *stream) {
-    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(o->device));
-    hipStream_t s = static_cast<hipStream_t>(stream);
+// One optimize_raw call's launch arguments (the momentum buffer of `name`,
+// created zeroed on its first call: sgd.cpp:40-47; the iteration count).
+static int sgd_prepare(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len, hipStream_t s,
+                       stg::SgdLaunch *out) {
     bool first = false;
     float *mom = nullptr;
     {
@@ -1024,13 +1023,9 @@ int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, u
         }
         o->iter++;  // sgd.cpp:262
     }
-    stg::SgdLaunch a;
+    stg::SgdLaunch a{};
     a.param = d_param;
     a.param_len = param_len;
-    a.grad = d_grad;
-    a.gidx = d_idx;
-    a.grad_len = grad_len;
-    a.d_grad_len = d_grad_len;
     a.mom = mom;
     a.first = first;
     a.momentum = o->momentum;
@@ -1038,8 +1033,42 @@ int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, u
     a.weight_decay = o->weight_decay;
     a.lr = o->maximize ? -(double)o->lr : (double)o->lr;  // sgd.cpp:51
     a.nesterov = o->nesterov;
+    *out = a;
+    return STG_OK;
+}
+
+int stg_sgd_optimize_raw_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len, const float *d_grad,
+                                const uint32_t *d_idx, uint32_t grad_len, const uint32_t *d_grad_len, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    stg::SgdLaunch a;
+    int rc = sgd_prepare(o, name, d_param, param_len, s, &a);
+    if (rc) return rc;
+    a.grad = d_grad;
+    a.gidx = d_idx;
+    a.grad_len = grad_len;
+    a.d_grad_len = d_grad_len;
     if (grad_len) HIP_TRY(stg::launch_sgd(a, s));
     return STG_OK;
+}
+
+int stg_merge_optimize_sgd_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len,
+                                  const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
+                                  float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
+                                  uint32_t *d_out_count, void *stream) {
+    // the decompress, then the step over its output (count read on the device).
+    // Fusing the step into the world-1 emission launch measured slower (55.5
+    // against 49.0 us per C5 step): its 41 tiles keep too few of the step's
+    // random read-modify-writes in flight.
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    int rc = stg_scatter_merge_device(d_idx, d_val, per_rank, world, param_len, d_dense, d_mark, d_out_idx, d_out_val,
+                                      d_out_count, stream);
+    if (rc) return rc;
+    const size_t cap = per_rank * (size_t)world;
+    return stg_sgd_optimize_raw_device(o, name, d_param, param_len, d_out_val, d_out_idx,
+                                       (uint32_t)std::min<size_t>(cap, 0xffffffffu), d_out_count, stream);
 }
 
 int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_t len, void *stream) {

@@ -290,6 +290,34 @@ class SparseSGD:
             C.c_void_p(gidx.data_ptr()), n, C.c_void_p(d_grad_len.data_ptr()) if d_grad_len is not None else None,
             C.c_void_p(torch.cuda.current_stream(param.device.index).cuda_stream)))
 
+    def merge_optimize(self, param, name: str, idx, val, per_rank: int, world: int = 1, dense=None, mark=None,
+                       out_idx=None, out_val=None, count=None):
+        """ModuleCpuOptimize::run (cpu_optimize.cpp:26-100): the MERGE
+        decompress of ``world`` rank streams of ``per_rank`` pairs into the
+        merged stream (returned, as ``scatter_merge``), then optimize_raw on it,
+        its length taken from the count on the device."""
+        import torch
+        dev, n = param.device, param.numel()
+        if out_idx is None:
+            out_idx = torch.empty(per_rank * world, dtype=torch.int32, device=dev)
+        if out_val is None:
+            out_val = torch.empty(per_rank * world, dtype=torch.float32, device=dev)
+        if count is None:
+            count = torch.empty(1, dtype=torch.int32, device=dev)
+        if world > 1:
+            if dense is None:
+                dense = torch.zeros(n, dtype=torch.float32, device=dev)
+            if mark is None:
+                mark = torch.zeros(n, dtype=torch.uint8, device=dev)
+        dp = C.c_void_p(dense.data_ptr()) if dense is not None else None
+        mp = C.c_void_p(mark.data_ptr()) if mark is not None else None
+        check(lib().stg_merge_optimize_sgd_device(
+            self._h, name.encode(), C.c_void_p(param.data_ptr()), n, C.c_void_p(idx.data_ptr()),
+            C.c_void_p(val.data_ptr()), per_rank, world, dp, mp, C.c_void_p(out_idx.data_ptr()),
+            C.c_void_p(out_val.data_ptr()), C.c_void_p(count.data_ptr()),
+            C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+        return out_idx, out_val, count
+
     def momentum_buffer(self, name: str, n: int):
         import torch
         out = np.zeros(n, np.float32)

@@ -173,6 +173,51 @@ def test_round_trip_compress_decompress_sgd(gpu, oracle, n, dist, param):
     oracle.sgd_free(hs)
 
 
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("opt", SGD_CASES[:2], ids=lambda o: f"m{o['momentum']}_n{int(o['nesterov'])}")
+def test_merge_optimize_sgd_fused(gpu, oracle, world, opt):
+    """ModuleCpuOptimize::run in one call (cpu_optimize.cpp:26-100): the merged
+    stream, the parameters and the momentum equal the oracle's decompress +
+    optimize_raw bit for bit over three iterations, world 1 and 2."""
+    import torch
+    from stellatrain_amd import SparseSGD, ThresholdvCompressor16, merge_numel
+    n = (1 << 20) + 5
+    k = merge_numel(n, 0.99)
+    comp = ThresholdvCompressor16()
+    sgd = SparseSGD(**opt)
+    hc, hs = oracle.tv16_new(), oracle.sgd_new(**opt)
+    param0 = synth(n, seed_for(23, 98)) * np.float32(1000)
+    po, pg = param0.copy(), torch.from_numpy(param0.copy()).to(gpu)
+    for it in range(3):
+        ios, vos, igs, vgs = [], [], [], []
+        for r in range(world):  # each rank's stream (the same codec, one key per rank)
+            src = synth(n, seed_for(17 + r, it))
+            co, io, vo = oracle.tv16_compress(hc, f"m{r}@weight", src, k)
+            idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+            val = torch.zeros(k, dtype=torch.float32, device=gpu)
+            assert comp.compress(f"m{r}@weight", torch.from_numpy(src).to(gpu), k, idx, val) == co
+            ios.append(io[:k]); vos.append(vo[:k]); igs.append(idx); vgs.append(val)
+        mi, mv = oracle.merge_decompress(np.concatenate(ios), np.concatenate(vos), k, world, n)
+        oracle.sgd_apply(hs, "m@weight", po, mv, mi)
+        oi, ov, cnt = sgd.merge_optimize(pg, "m@weight", torch.cat(igs), torch.cat(vgs), k, world)
+        m = int(cnt.item())
+        assert m == mi.size
+        gi, gv = oi[:m].cpu().numpy().view(np.uint32), ov[:m].cpu().numpy()
+        ei, ev = _sorted_pairs(gi, gv)
+        xi, xv = _sorted_pairs(mi.astype(np.uint32), mv)
+        assert np.array_equal(ei, xi) and np.array_equal(ev.view(np.uint32), xv.view(np.uint32))
+        got = pg.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), po.view(np.uint32)), f"param differs at iteration {it}"
+    mo = oracle.sgd_momentum(hs, "m@weight", n)
+    mg = sgd.momentum_buffer("m@weight", n)
+    if mo is None:
+        assert mg is None
+    else:
+        assert np.array_equal(mg.view(np.uint32), mo.view(np.uint32))
+    oracle.tv16_free(hc)
+    oracle.sgd_free(hs)
+
+
 def test_error_feedback_residual(gpu, oracle):
     """compress.cpp:172-186: after compress, src[idx[i]] = 0 for every slot
     i < numel and the bucket is copied into the residual."""

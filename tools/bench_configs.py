@@ -264,7 +264,10 @@ def c5_round_trip(torch, steps, kind="sgd"):
     for i, p in enumerate(params):
         fill(lib(), p, 777 + i, st.cuda_stream)
     comp = ThresholdvCompressor16()
-    sgd, label = make_opt(kind)
+    fused = kind == "sgd_fused"
+    sgd, label = make_opt("sgd" if fused else kind)
+    if fused:
+        label += ", one merge_optimize call"
     idx = torch.zeros(k, dtype=torch.int32, device=dev)
     val = torch.zeros(k, dtype=torch.float32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -275,6 +278,9 @@ def c5_round_trip(torch, steps, kind="sgd"):
     def step(s):
         j = s % nb
         comp.compress_async(f"{j}@w", grads[j], k, idx, val, count=cnt)
+        if fused:  # ModuleCpuOptimize::run in one call (SparseSGD.merge_optimize)
+            sgd.merge_optimize(params[j], f"{j}@w", idx, val, k, 1, out_idx=oi, out_val=ov, count=oc)
+            return
         scatter_merge(idx, val, k, 1, n, out_idx=oi, out_val=ov, count=oc)
         sgd.optimize_raw(params[j], f"{j}@w", ov, oi, grad_len=k, d_grad_len=oc)
     for s in range(2 * nb):
@@ -289,7 +295,7 @@ def c5_round_trip(torch, steps, kind="sgd"):
     e1.record(st)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / steps
-    alg = 4.0 * n + 8.0 * k + (16.0 if kind == "sgd" else 24.0) * k
+    alg = 4.0 * n + 8.0 * k + (24.0 if kind.startswith("adam") else 16.0) * k
     return {"config": f"C5 thresholdv16 compress + decompress + {label} 64 MiB k={k}", "us_per_step": round(us, 2),
             "host_enqueue_us_per_step": round(host_us, 2),
             "GBps_dense_in": round(4.0 * n / us / 1e3, 1), "alg_GBps": round(alg / us / 1e3, 1)}
@@ -555,7 +561,7 @@ def main():
     if "single" in only:  # one 64 MiB bucket per call, one stream: the latency of a lone call
         emit(time_device(torch, make_compressor("thresholdv16"), "thresholdv16 single-bucket", 64, 0.99, a.calls, 8, 16))
     if "c5" in only:
-        for kind in ("sgd", "adam", "adam_ams"):
+        for kind in ("sgd", "sgd_fused", "adam", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))
     if "gather" in only:
         for d in gather(torch, a.calls):
