@@ -40,6 +40,7 @@
 //   Indices are unique within a call (codec output / MERGE union), so the
 //   elements are independent apart from vmax.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ws.h"
 
@@ -205,27 +206,33 @@ static_assert(WPER == 16, "four uint4 of indices per lane");
 // Every load is issued before any is used -- the 16 index loads together,
 // then the 16 winner words (clamped addresses, results masked) -- two round
 // trips per lane instead of 32 dependent ones.
-__device__ __forceinline__ uint32_t win_keep(const uint32_t *__restrict__ idx, size_t m, size_t n,
-                                             const uint32_t *__restrict__ win, size_t e, uint32_t (&j)[WPER]) {
-    if (e + WPER <= m && (reinterpret_cast<uintptr_t>(idx + e) & 15u) == 0) {
+template <uint32_t WP>
+__device__ __forceinline__ uint32_t win_keep_t(const uint32_t *__restrict__ idx, size_t m, size_t n,
+                                               const uint32_t *__restrict__ win, size_t e, uint32_t (&j)[WP]) {
+    static_assert(WP % 4 == 0, "uint4 groups of indices");
+    if (e + WP <= m && (reinterpret_cast<uintptr_t>(idx + e) & 15u) == 0) {
         const uint4 *p = reinterpret_cast<const uint4 *>(idx + e);
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
+        for (uint32_t q = 0; q < WP / 4; ++q) {
             const uint4 v = p[q];
             j[4 * q] = v.x; j[4 * q + 1] = v.y; j[4 * q + 2] = v.z; j[4 * q + 3] = v.w;
         }
     } else {
 #pragma unroll
-        for (uint32_t b = 0; b < WPER; ++b) j[b] = idx[std::min<size_t>(e + b, m - 1)];
+        for (uint32_t b = 0; b < WP; ++b) j[b] = idx[std::min<size_t>(e + b, m - 1)];
     }
-    uint32_t w[WPER];
+    uint32_t w[WP];
 #pragma unroll
-    for (uint32_t b = 0; b < WPER; ++b) w[b] = win[j[b] < n ? j[b] : 0u];
+    for (uint32_t b = 0; b < WP; ++b) w[b] = win[j[b] < n ? j[b] : 0u];
     uint32_t keep = 0;
 #pragma unroll
-    for (uint32_t b = 0; b < WPER; ++b)
+    for (uint32_t b = 0; b < WP; ++b)
         if (e + b < m && j[b] < n && w[b] == (uint32_t)(e + b) + 1u) keep |= 1u << b;
     return keep;
+}
+__device__ __forceinline__ uint32_t win_keep(const uint32_t *__restrict__ idx, size_t m, size_t n,
+                                             const uint32_t *__restrict__ win, size_t e, uint32_t (&j)[WPER]) {
+    return win_keep_t<WPER>(idx, m, n, win, e, j);
 }
 
 __global__ void __launch_bounds__(STG_WG) win_count(const uint32_t *__restrict__ idx, size_t m, size_t n,
@@ -315,50 +322,58 @@ struct Win1Args {
     uint32_t *fail;     // sticky failure word: a tile whose look-back gave up
 };
 
+// WP pairs per lane: 4 (the default; 1,024-pair tiles, four times the
+// workgroups and the gathers of 16) or 16 (4,096-pair tiles: 41 workgroups at
+// 167,772 pairs, 13 us per call in the C5 kernel trace).
+template <uint32_t WP>
 __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     __shared__ uint32_t sh[STG_WAVES + 1];
     __shared__ uint32_t s_tile, s_bad;
-    __shared__ uint64_t s_P;
+    __shared__ uint64_t s_P, s_psum[STG_WAVES];
     const uint32_t tid = threadIdx.x, lane = __lane_id();
     if (tid == 0) { s_tile = (uint32_t)(g_add(a.ticket, 1ull) - a.base); s_bad = 0; }
     __syncthreads();
     const uint32_t tile = s_tile;
-    const size_t e = (size_t)tile * MARK_TILE + (size_t)WPER * tid;
-    uint32_t j[WPER];
-    const uint32_t keep = e < a.m ? win_keep(a.idx, a.m, a.n, a.win, e, j) : 0u;
-    float v[WPER];
-    if (e + WPER <= a.m && (reinterpret_cast<uintptr_t>(a.val + e) & 15u) == 0) {
+    const size_t e = (size_t)tile * (WP * STG_WG) + (size_t)WP * tid;
+    uint32_t j[WP];
+    const uint32_t keep = e < a.m ? win_keep_t<WP>(a.idx, a.m, a.n, a.win, e, j) : 0u;
+    float v[WP];
+    if (e + WP <= a.m && (reinterpret_cast<uintptr_t>(a.val + e) & 15u) == 0) {
         const float4 *p = reinterpret_cast<const float4 *>(a.val + e);
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
+        for (uint32_t q = 0; q < WP / 4; ++q) {
             const float4 x = p[q];
             v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
         }
     } else {
 #pragma unroll
-        for (uint32_t b = 0; b < WPER; ++b) v[b] = a.m ? a.val[std::min<size_t>(e + b, a.m - 1)] : 0.f;
+        for (uint32_t b = 0; b < WP; ++b) v[b] = a.m ? a.val[std::min<size_t>(e + b, a.m - 1)] : 0.f;
     }
     uint32_t tc;
     uint32_t r = wg_excl_scan((uint32_t)__popc(keep), sh, &tc);
     if (tid == 0) st_sc1(&a.desc[tile], ((uint64_t)a.tag << 32) | tc);
-    if (tid < 64) {  // look-back over tiles 0 .. tile-1, 64 per round trip
-        uint64_t P = 0;
-        for (uint32_t i0 = 0; i0 < tile; i0 += 64) {
-            const uint32_t i = i0 + lane;
+    {   // look-back over tiles 0 .. tile-1, STG_WG per round trip
+        uint64_t Pl = 0;
+        bool gave = false;
+        for (uint32_t i0 = 0; i0 < tile; i0 += STG_WG) {
+            const uint32_t i = i0 + tid;
             uint64_t d = i < tile ? ld_sc1(&a.desc[i]) : 0ull;
-            bool pend = i < tile && (uint32_t)(d >> 32) != a.tag;
-            for (uint32_t spins = 0; __ballot(pend); ++spins) {
+            for (uint32_t spins = 0; i < tile && (uint32_t)(d >> 32) != a.tag; ++spins) {
                 __builtin_amdgcn_s_sleep(4);
-                if (pend) {
-                    d = ld_sc1(&a.desc[i]);
-                    pend = (uint32_t)(d >> 32) != a.tag;
-                }
-                if (spins > (1u << 20)) { if (lane == 0) s_bad = 1; break; }  // ~0.3 s: give up, poison the count
+                d = ld_sc1(&a.desc[i]);
+                if (spins > (1u << 20)) { gave = true; break; }  // ~0.3 s: give up, poison the count
             }
-            P += (uint32_t)d;
+            Pl += (uint32_t)d;
         }
-        P = wave_sum64(P);
-        if (lane == 0) s_P = P;
+        if (gave) s_bad = 1;
+        Pl = wave_sum64(Pl);
+        if (lane == 0) s_psum[tid >> 6] = Pl;
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t t2 = 0;
+            for (uint32_t w = 0; w < STG_WAVES; ++w) t2 += s_psum[w];
+            s_P = t2;
+        }
     }
     __syncthreads();
     const uint64_t P = s_P;
@@ -369,7 +384,7 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     // tile that gave up first
     if (bad && tid == 0) g_or(a.fail, FAIL_SPIN_TIMEOUT);
 #pragma unroll
-    for (uint32_t b = 0; b < WPER; ++b) {
+    for (uint32_t b = 0; b < WP; ++b) {
         if (keep >> b & 1u) {
             if (!bad) {
                 a.out_idx[P + r] = j[b];
@@ -621,10 +636,13 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
         win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win);
         const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
         if (w1.desc) {  // count and emit in one launch (tagged tile counts, look-back)
-            Win1Args a{idx, val, per_rank, n, nt, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count,
+            static const uint32_t wp = getenv("STG_MERGE_WP") && atoi(getenv("STG_MERGE_WP")) == 16 ? 16u : 4u;
+            const uint32_t nt1 = (uint32_t)((per_rank + wp * STG_WG - 1) / (wp * STG_WG));
+            Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count,
                        w1.fail};
-            win_emit1t<<<nt, STG_WG, 0, s>>>(a);
-            if (w1.grid_out) *w1.grid_out = nt;
+            if (wp == 16) win_emit1t<16><<<nt1, STG_WG, 0, s>>>(a);
+            else win_emit1t<4><<<nt1, STG_WG, 0, s>>>(a);
+            if (w1.grid_out) *w1.grid_out = nt1;
             return hipGetLastError();
         }
         win_count<<<nt, STG_WG, 0, s>>>(idx, per_rank, n, win, scratch_tiles);
