@@ -209,8 +209,7 @@ static_assert(WPER == 16, "four uint4 of indices per lane");
 template <uint32_t WP>
 __device__ __forceinline__ uint32_t win_keep_t(const uint32_t *__restrict__ idx, size_t m, size_t n,
                                                const uint32_t *__restrict__ win, size_t e, uint32_t (&j)[WP]) {
-    static_assert(WP % 4 == 0, "uint4 groups of indices");
-    if (e + WP <= m && (reinterpret_cast<uintptr_t>(idx + e) & 15u) == 0) {
+    if (WP % 4 == 0 && e + WP <= m && (reinterpret_cast<uintptr_t>(idx + e) & 15u) == 0) {
         const uint4 *p = reinterpret_cast<const uint4 *>(idx + e);
 #pragma unroll
         for (uint32_t q = 0; q < WP / 4; ++q) {
@@ -338,7 +337,7 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     uint32_t j[WP];
     const uint32_t keep = e < a.m ? win_keep_t<WP>(a.idx, a.m, a.n, a.win, e, j) : 0u;
     float v[WP];
-    if (e + WP <= a.m && (reinterpret_cast<uintptr_t>(a.val + e) & 15u) == 0) {
+    if (WP % 4 == 0 && e + WP <= a.m && (reinterpret_cast<uintptr_t>(a.val + e) & 15u) == 0) {
         const float4 *p = reinterpret_cast<const float4 *>(a.val + e);
 #pragma unroll
         for (uint32_t q = 0; q < WP / 4; ++q) {
@@ -636,11 +635,16 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
         win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win);
         const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
         if (w1.desc) {  // count and emit in one launch (tagged tile counts, look-back)
-            static const uint32_t wp = getenv("STG_MERGE_WP") && atoi(getenv("STG_MERGE_WP")) == 16 ? 16u : 4u;
+            static const uint32_t wp = [] {
+                const int x = getenv("STG_MERGE_WP") ? atoi(getenv("STG_MERGE_WP")) : 4;
+                return x == 16 ? 16u : x == 2 ? 2u : x == 1 ? 1u : 4u;
+            }();
             const uint32_t nt1 = (uint32_t)((per_rank + wp * STG_WG - 1) / (wp * STG_WG));
             Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count,
                        w1.fail};
             if (wp == 16) win_emit1t<16><<<nt1, STG_WG, 0, s>>>(a);
+            else if (wp == 2) win_emit1t<2><<<nt1, STG_WG, 0, s>>>(a);
+            else if (wp == 1) win_emit1t<1><<<nt1, STG_WG, 0, s>>>(a);
             else win_emit1t<4><<<nt1, STG_WG, 0, s>>>(a);
             if (w1.grid_out) *w1.grid_out = nt1;
             return hipGetLastError();

@@ -600,9 +600,9 @@ MergeScratch *merge_scratch(int dev, hipStream_t s) {
 // Caller holds m->mu.
 int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_rank, int world) {
     // per-tile counts and their prefixes (the world > 1 mark scan)
-    // ... and the world-1 emission's tagged tile counts (tiles of MERGE_TILE / 4 pairs)
+    // ... and the world-1 emission's tagged tile counts (tiles of >= MERGE_TILE / 16 pairs)
     const size_t tiles = std::max(2 * ((std::max(n, per_rank) + stg::MERGE_TILE - 1) / stg::MERGE_TILE) + 2,
-                                  (per_rank + stg::MERGE_TILE / 4 - 1) / (stg::MERGE_TILE / 4) + 2);
+                                  (per_rank + stg::MERGE_TILE / 16 - 1) / (stg::MERGE_TILE / 16) + 2);
     if (tiles > m->cap_tiles) {
         HIP_TRY(hipStreamSynchronize(s));
         (void)hipFree(m->tiles);

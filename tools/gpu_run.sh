@@ -52,8 +52,9 @@ for s in "$@"; do
         prof_topk) step prof_topk 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_topk" -o run -- python3 tools/bench_configs.py --only topk --cpu-seconds 0
             python3 tools/ktrace.py gpurun_out/prof_topk > gpurun_out/prof_topk.txt 2>&1 ;;
         c5ab)  # world-1 MERGE emission: 1,024-pair tiles (default) against 4,096 (STG_MERGE_WP=16)
-            STG_MERGE_WP=16 step c5_wp16 150 python tools/bench_configs.py --only c5 --cpu-seconds 0
-            step c5_wp4 150 python tools/bench_configs.py --only c5 --cpu-seconds 0 ;;
+            for W in 16 4 2 1; do
+                STG_MERGE_WP=$W step c5_wp$W 150 python tools/bench_configs.py --only c5 --cpu-seconds 0
+            done ;;
         prof_c5) step prof_c5 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c5" -o run -- python3 tools/bench_configs.py --only c5
             python3 tools/ktrace.py gpurun_out/prof_c5 24 > gpurun_out/prof_c5.txt 2>&1 ;;
         c2ab)  # shipped-mode top-k: the ordered six-launch path (STG_TOPK_BK=0) against the unordered three
