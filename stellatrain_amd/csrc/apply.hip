@@ -520,7 +520,7 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
 // lower block ids, so they are dispatched first and always finish publishing;
 // the poll is still bounded.  The last tile stores the call's vmax.
 __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t tag) {
-    __shared__ uint32_t sh[STG_WAVES];
+    __shared__ uint32_t sh[STG_WAVES], s_lb[STG_WAVES];
     __shared__ uint32_t s_pre;
     const uint32_t len = adam_len(a);
     const uint32_t ntile = (len + ADAM_TILE - 1) / ADAM_TILE;
@@ -554,26 +554,29 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
     for (uint32_t w = 0; w < STG_WAVES; ++w) tile_max = max(tile_max, sh[w]);
     uint64_t *words = reinterpret_cast<uint64_t *>(a.tiles);
     if (threadIdx.x == 0) st_sc1(&words[tile], ((uint64_t)tag << 32) | tile_max);
-    // look-back by wave 0: 64 predecessors per round
-    if (threadIdx.x < 64) {
-        uint32_t pre = vmax0;
-        for (uint32_t p0 = 0; p0 < tile; p0 += 64) {
-            const uint32_t p = p0 + threadIdx.x;
-            if (p < tile) {
-                uint64_t w = ld_sc1(&words[p]);
-                for (uint32_t spins = 0; (uint32_t)(w >> 32) != tag; ++spins) {
-                    if (spins >= (1u << 22)) {  // starved predecessor: flag it (stg_adam_check), never use a stale word silently
-                        g_or(a.fail, FAIL_SPIN_TIMEOUT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    w = ld_sc1(&words[p]);
+    // look-back by the whole workgroup: STG_WG predecessors per round trip
+    {
+        uint32_t pt = vmax0;
+        for (uint32_t p = threadIdx.x; p < tile; p += STG_WG) {
+            uint64_t w = ld_sc1(&words[p]);
+            for (uint32_t spins = 0; (uint32_t)(w >> 32) != tag; ++spins) {
+                if (spins >= (1u << 22)) {  // starved predecessor: flag it (stg_adam_check), never use a stale word silently
+                    g_or(a.fail, FAIL_SPIN_TIMEOUT);
+                    break;
                 }
-                pre = max(pre, (uint32_t)w);
+                __builtin_amdgcn_s_sleep(1);
+                w = ld_sc1(&words[p]);
             }
+            pt = max(pt, (uint32_t)w);
         }
-        pre = wave_max(pre);
-        if (threadIdx.x == 0) s_pre = pre;
+        pt = wave_max(pt);
+        if (__lane_id() == 0) s_lb[threadIdx.x >> 6] = pt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t m = 0;
+            for (uint32_t w = 0; w < STG_WAVES; ++w) m = max(m, s_lb[w]);
+            s_pre = m;
+        }
     }
     __syncthreads();
     uint32_t pre = s_pre;
