@@ -122,10 +122,13 @@ def test_python_threads_device_streams(gpu, oracle):
             outs = []
             barrier.wait()
             for c in range(calls):
-                idx = torch.zeros(k, dtype=torch.int32, device=gpu)
-                val = torch.zeros(k, dtype=torch.float32, device=gpu)
-                cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
+                # the outputs are zeroed on the thread's stream too: torch's
+                # streams do not wait for the default stream, so zeros issued
+                # there could land after the call's writes
                 with torch.cuda.stream(s):
+                    idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+                    val = torch.zeros(k, dtype=torch.float32, device=gpu)
+                    cnt = torch.zeros(1, dtype=torch.int32, device=gpu)
                     check(lib().stg_synth_fill_device(C.c_void_p(src.data_ptr()), n, 7000 * (t + 1) + c, 0, 0,
                                                       C.c_void_p(s.cuda_stream)))
                     comp.compress_raw(f"py{t}@w".encode(), src.data_ptr(), n, k, idx.data_ptr(), k, val.data_ptr(),
