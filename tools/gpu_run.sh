@@ -59,6 +59,7 @@ for s in "$@"; do
             python3 tools/ktrace.py gpurun_out/prof_c5 24 > gpurun_out/prof_c5.txt 2>&1 ;;
         prof_merge) step prof_merge 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_merge" -o run -- python3 tools/bench_configs.py --only merge
             python3 tools/ktrace.py gpurun_out/prof_merge 16 > gpurun_out/prof_merge.txt 2>&1 ;;
+        scale_drop) step scale_drop 280 python tools/scale_drop.py 4 ;;
         c2ab)  # shipped-mode top-k: the ordered six-launch path (STG_TOPK_BK=0) against the unordered three
             STG_TOPK_BK=0 step c2_ordered 150 python tools/bench_configs.py --only topk --cpu-seconds 0
             step c2_bk 150 python tools/bench_configs.py --only topk --cpu-seconds 0
