@@ -52,12 +52,20 @@ constexpr uint32_t MARK_TILE = MERGE_TILE;  // marks (or pairs) per tile (one ui
 
 // Winner election: win[j] = 1 + the last position of index j in the rank's
 // stream (indices >= n are dropped: the reference would throw on them).
+// With `dup` (world 1): any repeated or out-of-range index sets it (the
+// emission then elects; otherwise every pair is its index's only occurrence and
+// the emission copies the stream), and the emission's tile ticket starts at 0.
 __global__ void __launch_bounds__(STG_WG) win_mark(const uint32_t *__restrict__ idx, size_t m, size_t n,
-                                                   uint32_t *__restrict__ win) {
+                                                   uint32_t *__restrict__ win, uint32_t *dup, uint64_t *ticket) {
+    if (ticket && blockIdx.x == 0 && threadIdx.x == 0) st_sc1(ticket, 0ull);
     const size_t stride = (size_t)gridDim.x * STG_WG;
     for (size_t i = (size_t)blockIdx.x * STG_WG + threadIdx.x; i < m; i += stride) {
         const uint32_t j = idx[i];
-        if (j < n) atomicMax(&win[j], (uint32_t)i + 1u);
+        if (!dup) {
+            if (j < n) atomicMax(&win[j], (uint32_t)i + 1u);
+        } else if (j >= n || atomicMax(&win[j], (uint32_t)i + 1u) != 0u) {
+            g_or(dup, 1u);  // rare for codec output: its indices are unique
+        }
     }
 }
 
@@ -319,6 +327,7 @@ struct Win1Args {
     float *out_val;
     uint32_t *out_count;
     uint32_t *fail;     // sticky failure word: a tile whose look-back gave up
+    uint32_t *dup;      // set by win_mark when an index repeats (or is >= n); zeroed by the last tile then
 };
 
 // WP pairs per lane: 4 (the default; 1,024-pair tiles, four times the
@@ -329,7 +338,47 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     __shared__ uint32_t sh[STG_WAVES + 1];
     __shared__ uint32_t s_tile, s_bad;
     __shared__ uint64_t s_P, s_psum[STG_WAVES];
+    __shared__ uint32_t s_dup;
     const uint32_t tid = threadIdx.x, lane = __lane_id();
+    if (tid == 0) s_dup = ld_sc1(a.dup);
+    __syncthreads();
+    if (!s_dup) {
+        // no index repeats: every pair wins and keeps its place, so the output
+        // is the stream itself -- no ticket, no look-back (tile = block)
+        const size_t e = (size_t)blockIdx.x * (WP * STG_WG) + (size_t)WP * tid;
+        uint32_t j[WP];
+        float v[WP];
+        if (WP % 4 == 0 && e + WP <= a.m && (reinterpret_cast<uintptr_t>(a.idx + e) & 15u) == 0 &&
+            (reinterpret_cast<uintptr_t>(a.val + e) & 15u) == 0) {
+#pragma unroll
+            for (uint32_t q = 0; q < WP / 4; ++q) {
+                const uint4 x = reinterpret_cast<const uint4 *>(a.idx + e)[q];
+                const float4 y = reinterpret_cast<const float4 *>(a.val + e)[q];
+                j[4 * q] = x.x; j[4 * q + 1] = x.y; j[4 * q + 2] = x.z; j[4 * q + 3] = x.w;
+                v[4 * q] = y.x; v[4 * q + 1] = y.y; v[4 * q + 2] = y.z; v[4 * q + 3] = y.w;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t b = 0; b < WP; ++b) {
+                const size_t i = std::min<size_t>(e + b, a.m ? a.m - 1 : 0);
+                j[b] = a.idx[i];
+                v[b] = a.val[i];
+            }
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < WP; ++b) {
+            if (e + b < a.m) {
+                a.out_idx[e + b] = j[b];
+                a.out_val[e + b] = (0.0f + v[b]) / 1.0f;
+                a.win[j[b]] = 0;  // scratch back to zero for the next call
+            }
+        }
+        if (tid == 0 && blockIdx.x == a.ntiles - 1) {
+            __builtin_amdgcn_s_waitcnt(0);
+            *a.out_count = ld_sc1(a.fail) ? 0xffffffffu : (uint32_t)a.m;
+        }
+        return;
+    }
     if (tid == 0) { s_tile = (uint32_t)(g_add(a.ticket, 1ull) - a.base); s_bad = 0; }
     __syncthreads();
     const uint32_t tile = s_tile;
@@ -396,6 +445,9 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     if (tid == 0 && tile == a.ntiles - 1) {
         __builtin_amdgcn_s_waitcnt(0);
         *a.out_count = (bad || ld_sc1(a.fail)) ? 0xffffffffu : (uint32_t)(P + tc);
+        // every tile read the flag before publishing its count (the look-back
+        // above saw them all): clear it for the next call
+        if (!bad) st_sc1(a.dup, 0u);
     }
 }
 
@@ -635,7 +687,8 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
                                                                           (size_t)num_cu * 8));
     if (world == 1) {
         if (!per_rank) return hipMemsetAsync(out_count, 0, sizeof(uint32_t), s);
-        win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win);
+        win_mark<<<blocks, STG_WG, 0, s>>>(idx, per_rank, n, win, w1.desc ? w1.dup : nullptr,
+                                           w1.desc ? w1.ticket : nullptr);
         const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
         if (w1.desc) {  // count and emit in one launch (tagged tile counts, look-back)
             static const uint32_t wp = [] {
@@ -643,8 +696,8 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
                 return x == 16 ? 16u : x == 2 ? 2u : x == 1 ? 1u : 4u;
             }();
             const uint32_t nt1 = (uint32_t)((per_rank + wp * STG_WG - 1) / (wp * STG_WG));
-            Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, w1.base, w1.tag, out_idx, out_val, out_count,
-                       w1.fail};
+            Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, 0ull /* win_mark zeroed it */, w1.tag,
+                       out_idx, out_val, out_count, w1.fail, w1.dup};
             if (wp == 16) win_emit1t<16><<<nt1, STG_WG, 0, s>>>(a);
             else if (wp == 2) win_emit1t<2><<<nt1, STG_WG, 0, s>>>(a);
             else if (wp == 1) win_emit1t<1><<<nt1, STG_WG, 0, s>>>(a);

@@ -573,9 +573,8 @@ struct MergeScratch {
     uint32_t *tiles = nullptr, *win = nullptr;
     size_t cap_tiles = 0, cap_win = 0;
     // world == 1 in one launch: tagged per-tile counts (cap_tiles of them, zeroed
-    // whenever reallocated), the tile ticket and its value at the next call
+    // whenever reallocated); the tile ticket and the duplicate flag
     uint64_t *desc = nullptr, *ticket = nullptr;
-    uint64_t tbase = 0;
     uint32_t tag = 0;
     uint32_t *fail = nullptr;  // sticky device failure word (a look-back that gave up)
     ~MergeScratch() {
@@ -614,10 +613,9 @@ int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_ra
         HIP_TRY(hipMemsetAsync(m->desc, 0, tiles * sizeof(uint64_t), s));  // no stale tags
         m->cap_tiles = tiles;
     }
-    if (!m->ticket) {
-        HIP_TRY(hipMalloc(&m->ticket, sizeof(uint64_t)));
-        HIP_TRY(hipMemsetAsync(m->ticket, 0, sizeof(uint64_t), s));
-        m->tbase = 0;
+    if (!m->ticket) {  // [0]: the emission's tile ticket; [1]: the duplicate flag (low word)
+        HIP_TRY(hipMalloc(&m->ticket, 2 * sizeof(uint64_t)));
+        HIP_TRY(hipMemsetAsync(m->ticket, 0, 2 * sizeof(uint64_t), s));
     }
     if (!m->fail) {
         HIP_TRY(hipMalloc(&m->fail, sizeof(uint32_t)));
@@ -932,10 +930,10 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
     if (rc) return rc;
     if (++ms->tag == 0) ms->tag = 1;
     uint32_t grid = 0;
-    const stg::Win1Desc w1{ms->desc, ms->ticket, ms->tbase, ms->tag, &grid, ms->fail};
+    const stg::Win1Desc w1{ms->desc, ms->ticket, 0, ms->tag, &grid, ms->fail,
+                           reinterpret_cast<uint32_t *>(ms->ticket + 1)};
     HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, n, d_dense, d_mark, d_out_idx, d_out_val,
                                       d_out_count, ms->tiles, ms->win, ncu, s, w1));
-    ms->tbase += grid;
     return STG_OK;
 }
 

@@ -252,11 +252,12 @@ hipError_t launch_synth(float *dst, size_t n, uint64_t seed, int dist, uint32_t 
 // two-launch count / emit instead)
 struct Win1Desc {
     uint64_t *desc;       // per tile {tag:32 | winners:32}, zero at creation
-    uint64_t *ticket;     // monotonic tile counter, zero at creation
-    uint64_t base;        // its value when the call starts
+    uint64_t *ticket;     // tile counter, zeroed by each call's win_mark
+    uint64_t base;        // unused (0)
     uint32_t tag;         // call tag >= 1
     uint32_t *grid_out;   // receives the tiles launched (the ticket advances by it)
     uint32_t *fail;       // sticky failure word of the scratch (a look-back that gave up)
+    uint32_t *dup;        // world 1: set when an index repeats; the ticket then counts from 0 (win_mark zeroes it)
 };
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,

@@ -76,6 +76,36 @@ def test_scatter_merge_parity(gpu, oracle, n, per_rank, world, overlap):
     scatter_merge_check()  # no device failure on this stream's scratch
 
 
+def test_scatter_merge_world1_duplicates(gpu, oracle):
+    """World 1 takes a copy path when no index repeats and the election path
+    when one does (csrc/apply.hip win_mark's duplicate flag): alternate
+    duplicate-free and duplicated streams on one stream's scratch, each against
+    the oracle (last occurrence wins, cpu_optimize.cpp:46-50), the flag cleared
+    between them."""
+    import torch
+    from stellatrain_amd import scatter_merge
+    from stellatrain_amd.engine import scatter_merge_check
+    n, per_rank = 100013, 20000
+    rng = np.random.default_rng(11)
+    for it, dups in enumerate([False, True, False, True, True, False]):
+        idx = rng.choice(n, per_rank, replace=False).astype(np.uint32)
+        if dups:  # every 7th pair repeats an earlier index of the stream
+            src = rng.integers(0, per_rank // 2, per_rank // 7)
+            idx[per_rank // 2:per_rank // 2 + src.size] = idx[src]
+        val = synth(per_rank, seed_for(61, it)) * np.float32(100)
+        oi, ov = oracle.merge_decompress(idx, val, per_rank, 1, n)
+        out_i, out_v, cnt = scatter_merge(torch.from_numpy(idx.view(np.int32)).to(gpu), torch.from_numpy(val).to(gpu),
+                                          per_rank, 1, n)
+        m = int(cnt.item())
+        assert m == oi.size, (it, dups)
+        gi, gv = _sorted_pairs(out_i[:m].cpu().numpy(), out_v[:m].cpu().numpy())
+        ei, ev = _sorted_pairs(oi, ov)
+        assert np.array_equal(gi, ei) and np.array_equal(gv.view(np.uint32), ev.view(np.uint32)), (it, dups)
+        if not dups:  # the copy path keeps the stream's order
+            assert np.array_equal(out_i[:m].cpu().numpy().view(np.uint32), idx)
+    scatter_merge_check()
+
+
 def test_scatter_merge_release_and_reuse(gpu, oracle):
     """The per-(device, stream) MERGE scratch can be released and is rebuilt
     by the next call on that stream (world 1: the one-launch look-back path)."""
