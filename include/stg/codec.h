@@ -184,8 +184,11 @@ int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_
 /* ModuleCpuOptimize::run (engine/modules/cpu_optimize.cpp:26-100): the MERGE
  * decompress of the received stream (as stg_scatter_merge_device: d_out_idx /
  * d_out_val / d_out_count get the merged stream, param_len is n) followed by
- * SparseOptimizer::optimize_raw of `o` on it (sgd.cpp:34-263), in one call,
- * stream-ordered, the step's length read from d_out_count on the device. */
+ * SparseOptimizer::optimize_raw of `o` on it (sgd.cpp:34-263), in one call.
+ * world == 1: two launches, the election and the emission with every winner's
+ * step in the same pass (each index is elected once, so the updates commute;
+ * parameters and momentum bitwise equal to the two separate calls); world > 1:
+ * the two calls, the step's length read from d_out_count on the device. */
 int stg_merge_optimize_sgd_device(stg_sgd_t o, const char *name, float *d_param, uint32_t param_len,
                                   const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
                                   float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,

@@ -313,6 +313,19 @@ __global__ void __launch_bounds__(STG_WG) win_emit1(const uint32_t *__restrict__
 // each publishes its winner count as a tagged word, sums the earlier tiles'
 // counts (look-back) and writes its winners at that offset; the last tile
 // writes the count.
+// SGD::optimize_raw on one element (optim/sgd.cpp:34-263, scalar path), with
+// param[id] = x and mom[id] = m loaded by the caller: the same expression as
+// sgd_apply, so a step fused into the emission agrees with it bitwise.
+__device__ __forceinline__ void sgd_step(const SgdLaunch &a, uint32_t id, float g, float x, float m) {
+    if (a.weight_decay != 0.f) g = fmaf(a.weight_decay, x, g);
+    if (a.mom) {
+        const float b = a.first ? g : fmaf(m, a.momentum, (1.0f - a.dampening) * g);
+        g = a.nesterov ? fmaf(a.momentum, b, g) : b;
+        a.mom[id] = b;
+    }
+    a.param[id] = (float)fma(-a.lr, (double)g, (double)x);
+}
+
 struct Win1Args {
     const uint32_t *idx;
     const float *val;
@@ -328,6 +341,8 @@ struct Win1Args {
     uint32_t *out_count;
     uint32_t *fail;     // sticky failure word: a tile whose look-back gave up
     uint32_t *dup;      // set by win_mark when an index repeats (or is >= n); zeroed by the last tile then
+    bool fuse_sgd;      // ModuleCpuOptimize::run: optimize_raw on every winner as it is emitted
+    SgdLaunch sgd;
 };
 
 // WP pairs per lane: 4 (the default; 1,024-pair tiles, four times the
@@ -365,11 +380,22 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
                 v[b] = a.val[i];
             }
         }
+        float xp[WP], mp[WP];
+        if (a.fuse_sgd) {  // every pair is a winner: its parameter and momentum words, loaded together
+#pragma unroll
+            for (uint32_t b = 0; b < WP; ++b) {
+                const uint32_t id = e + b < a.m ? j[b] : 0u;
+                xp[b] = a.sgd.param[id];
+                mp[b] = a.sgd.mom ? a.sgd.mom[id] : 0.f;
+            }
+        }
 #pragma unroll
         for (uint32_t b = 0; b < WP; ++b) {
             if (e + b < a.m) {
+                const float g = (0.0f + v[b]) / 1.0f;  // merged_grad[j] (cpu_optimize.cpp:49-55), world 1
                 a.out_idx[e + b] = j[b];
-                a.out_val[e + b] = (0.0f + v[b]) / 1.0f;
+                a.out_val[e + b] = g;
+                if (a.fuse_sgd) sgd_step(a.sgd, j[b], g, xp[b], mp[b]);  // indices unique: updates commute
                 a.win[j[b]] = 0;  // scratch back to zero for the next call
             }
         }
@@ -396,6 +422,15 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     } else {
 #pragma unroll
         for (uint32_t b = 0; b < WP; ++b) v[b] = a.m ? a.val[std::min<size_t>(e + b, a.m - 1)] : 0.f;
+    }
+    float xp[WP], mp[WP];
+    if (a.fuse_sgd) {  // the winners' parameter and momentum words, loaded under the look-back
+#pragma unroll
+        for (uint32_t b = 0; b < WP; ++b) {
+            const uint32_t id = (keep >> b & 1u) ? j[b] : 0u;
+            xp[b] = a.sgd.param[id];
+            mp[b] = a.sgd.mom ? a.sgd.mom[id] : 0.f;
+        }
     }
     uint32_t tc;
     uint32_t r = wg_excl_scan((uint32_t)__popc(keep), sh, &tc);
@@ -434,10 +469,12 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
 #pragma unroll
     for (uint32_t b = 0; b < WP; ++b) {
         if (keep >> b & 1u) {
+            const float g = (0.0f + v[b]) / 1.0f;
             if (!bad) {
                 a.out_idx[P + r] = j[b];
-                a.out_val[P + r] = (0.0f + v[b]) / 1.0f;
+                a.out_val[P + r] = g;
             }
+            if (a.fuse_sgd) sgd_step(a.sgd, j[b], g, xp[b], mp[b]);  // each index elected once: updates commute
             a.win[j[b]] = 0;  // scratch back to zero for the next call
             ++r;
         }
@@ -697,7 +734,8 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
             }();
             const uint32_t nt1 = (uint32_t)((per_rank + wp * STG_WG - 1) / (wp * STG_WG));
             Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, 0ull /* win_mark zeroed it */, w1.tag,
-                       out_idx, out_val, out_count, w1.fail, w1.dup};
+                       out_idx, out_val, out_count, w1.fail, w1.dup, w1.sgd != nullptr,
+                       w1.sgd ? *w1.sgd : SgdLaunch{}};
             if (wp == 16) win_emit1t<16><<<nt1, STG_WG, 0, s>>>(a);
             else if (wp == 2) win_emit1t<2><<<nt1, STG_WG, 0, s>>>(a);
             else if (wp == 1) win_emit1t<1><<<nt1, STG_WG, 0, s>>>(a);

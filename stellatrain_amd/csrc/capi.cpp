@@ -1057,18 +1057,36 @@ int stg_merge_optimize_sgd_device(stg_sgd_t o, const char *name, float *d_param,
                                   const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
                                   float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
                                   uint32_t *d_out_count, void *stream) {
-    // the decompress, then the step over its output (count read on the device).
-    // Fusing the step into the world-1 emission launch measured slower (55.5
-    // against 49.0 us per C5 step): its 41 tiles keep too few of the step's
-    // random read-modify-writes in flight.
     if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(o->device));
-    int rc = stg_scatter_merge_device(d_idx, d_val, per_rank, world, param_len, d_dense, d_mark, d_out_idx, d_out_val,
-                                      d_out_count, stream);
+    if (world != 1 || per_rank == 0) {  // the merge of several ranks, then the step over its output
+        int rc = stg_scatter_merge_device(d_idx, d_val, per_rank, world, param_len, d_dense, d_mark, d_out_idx,
+                                          d_out_val, d_out_count, stream);
+        if (rc) return rc;
+        const size_t cap = per_rank * (size_t)world;
+        return stg_sgd_optimize_raw_device(o, name, d_param, param_len, d_out_val, d_out_idx,
+                                           (uint32_t)std::min<size_t>(cap, 0xffffffffu), d_out_count, stream);
+    }
+    // world 1: the election, then the emission with every winner's step in the
+    // same pass (each index is elected once, so the updates commute)
+    if (per_rank >= (size_t(1) << 32) || param_len == 0)
+        return fail(STG_ERR_UNSUPPORTED, "more than 2^32-1 elements or an empty parameter");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    stg::SgdLaunch a;
+    int rc = sgd_prepare(o, name, d_param, param_len, s, &a);
     if (rc) return rc;
-    const size_t cap = per_rank * (size_t)world;
-    return stg_sgd_optimize_raw_device(o, name, d_param, param_len, d_out_val, d_out_idx,
-                                       (uint32_t)std::min<size_t>(cap, 0xffffffffu), d_out_count, stream);
+    int ncu = 256;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device));
+    MergeScratch *ms = merge_scratch(o->device, s);
+    std::lock_guard<std::mutex> g(ms->mu);
+    if ((rc = merge_scratch_ensure(ms, s, param_len, per_rank, world))) return rc;
+    if (++ms->tag == 0) ms->tag = 1;
+    uint32_t grid = 0;
+    stg::Win1Desc w1{ms->desc, ms->ticket, 0, ms->tag, &grid, ms->fail, reinterpret_cast<uint32_t *>(ms->ticket + 1)};
+    w1.sgd = &a;
+    HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, param_len, d_dense, d_mark, d_out_idx, d_out_val,
+                                      d_out_count, ms->tiles, ms->win, ncu, s, w1));
+    return STG_OK;
 }
 
 int stg_sgd_get_momentum(stg_sgd_t o, const char *name, float *host_out, uint32_t len, void *stream) {

@@ -294,8 +294,8 @@ class SparseSGD:
                        out_idx=None, out_val=None, count=None):
         """ModuleCpuOptimize::run (cpu_optimize.cpp:26-100): the MERGE
         decompress of ``world`` rank streams of ``per_rank`` pairs into the
-        merged stream (returned, as ``scatter_merge``), then optimize_raw on it,
-        its length taken from the count on the device."""
+        merged stream (returned, as ``scatter_merge``), then optimize_raw on it;
+        at world 1 the step runs inside the decompress's emission launch."""
         import torch
         dev, n = param.device, param.numel()
         if out_idx is None:

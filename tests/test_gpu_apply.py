@@ -208,7 +208,8 @@ def test_round_trip_compress_decompress_sgd(gpu, oracle, n, dist, param):
 def test_merge_optimize_sgd_fused(gpu, oracle, world, opt):
     """ModuleCpuOptimize::run in one call (cpu_optimize.cpp:26-100): the merged
     stream, the parameters and the momentum equal the oracle's decompress +
-    optimize_raw bit for bit over three iterations, world 1 and 2."""
+    optimize_raw bit for bit over three iterations (world 1: the step runs in
+    the emission launch; world 2: the two calls)."""
     import torch
     from stellatrain_amd import SparseSGD, ThresholdvCompressor16, merge_numel
     n = (1 << 20) + 5
@@ -245,6 +246,37 @@ def test_merge_optimize_sgd_fused(gpu, oracle, world, opt):
     else:
         assert np.array_equal(mg.view(np.uint32), mo.view(np.uint32))
     oracle.tv16_free(hc)
+    oracle.sgd_free(hs)
+
+
+def test_merge_optimize_sgd_world1_duplicates(gpu, oracle):
+    """The step fused into the world-1 emission on both of its paths: streams
+    with repeated indices (the election path) and without (the copy path),
+    alternating on one scratch; parameters and momentum bit-exact against the
+    oracle's decompress + optimize_raw."""
+    import torch
+    from stellatrain_amd import SparseSGD
+    n, per_rank = 100013, 20000
+    opt = dict(lr=0.05, momentum=0.9, dampening=0.1, weight_decay=1e-4, nesterov=True)
+    sgd = SparseSGD(**opt)
+    hs = oracle.sgd_new(**opt)
+    param0 = synth(n, seed_for(23, 97)) * np.float32(1000)
+    po, pg = param0.copy(), torch.from_numpy(param0.copy()).to(gpu)
+    rng = np.random.default_rng(12)
+    for it, dups in enumerate([True, False, True, False]):
+        idx = rng.choice(n, per_rank, replace=False).astype(np.uint32)
+        if dups:
+            src = rng.integers(0, per_rank // 2, per_rank // 7)
+            idx[per_rank // 2:per_rank // 2 + src.size] = idx[src]
+        val = synth(per_rank, seed_for(62, it)) * np.float32(100)
+        mi, mv = oracle.merge_decompress(idx, val, per_rank, 1, n)
+        oracle.sgd_apply(hs, "d@weight", po, mv, mi)
+        oi, ov, cnt = sgd.merge_optimize(pg, "d@weight", torch.from_numpy(idx.view(np.int32)).to(gpu),
+                                         torch.from_numpy(val).to(gpu), per_rank, 1)
+        assert int(cnt.item()) == mi.size, (it, dups)
+        assert np.array_equal(pg.cpu().numpy().view(np.uint32), po.view(np.uint32)), (it, dups)
+    mo = oracle.sgd_momentum(hs, "d@weight", n)
+    assert np.array_equal(sgd.momentum_buffer("d@weight", n).view(np.uint32), mo.view(np.uint32))
     oracle.sgd_free(hs)
 
 

@@ -267,7 +267,7 @@ def c5_round_trip(torch, steps, kind="sgd"):
     fused = kind == "sgd_fused"
     sgd, label = make_opt("sgd" if fused else kind)
     if fused:
-        label += ", one merge_optimize call"
+        label += ", one merge_optimize call (step fused into the decompress)"
     idx = torch.zeros(k, dtype=torch.int32, device=dev)
     val = torch.zeros(k, dtype=torch.float32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
