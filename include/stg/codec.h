@@ -193,6 +193,13 @@ int stg_merge_optimize_sgd_device(stg_sgd_t o, const char *name, float *d_param,
                                   const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
                                   float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
                                   uint32_t *d_out_count, void *stream);
+/* The same with Adam (adam.cpp:19-86): world 1 without amsgrad runs the step
+ * inside the emission launch; amsgrad (its running maximum is an ordered scan)
+ * and world > 1 run the decompress, then stg_adam_optimize_raw_device. */
+int stg_merge_optimize_adam_device(stg_adam_t o, const char *name, float *d_param, uint32_t param_len,
+                                   const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
+                                   float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
+                                   uint32_t *d_out_count, void *stream);
 
 /* Sparse Adam (optim/adam.cpp:19-86; options Adam::configure adam.cpp:90-122,
  * defaults adam.h:21-23, lr sparse_optimizer.h:30).  optimize_raw() keeps per

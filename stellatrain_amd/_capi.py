@@ -66,6 +66,9 @@ _SIGS = {
     "stg_merge_optimize_sgd_device": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                                 C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,
                                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "stg_merge_optimize_adam_device": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                                 C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "stg_adam_create": (C.c_int, [C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int,
                                   C.POINTER(C.c_void_p)]),
     "stg_adam_destroy": (C.c_int, [C.c_void_p]),

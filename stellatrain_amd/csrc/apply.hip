@@ -326,6 +326,21 @@ __device__ __forceinline__ void sgd_step(const SgdLaunch &a, uint32_t id, float 
     a.param[id] = (float)fma(-a.lr, (double)g, (double)x);
 }
 
+// Adam::optimize_raw on one element (optim/adam.cpp:19-86, no amsgrad), with
+// param[id] = x, m[id] = m0, v[id] = v0 loaded by the caller: the expressions of
+// adam_elem / adam_apply below, so a fused step agrees with them bitwise.
+__device__ __forceinline__ void adam_step(const AdamLaunch &a, uint32_t id, float g, float x, float m0, float v0) {
+    if (a.maximize) g = -g;
+    if (a.weight_decay != 0.f) g = fmaf(a.weight_decay, x, g);
+    const float mt = fmaf(a.b1, m0, (1.f - a.b1) * g);
+    const float vt = fmaf(a.b2, v0, ((1.f - a.b2) * g) * g);
+    const double num = ((double)mt / a.c1) * a.lr;
+    const double vt_hat = (double)vt / a.c2;
+    a.param[id] = (float)((double)x - num / ((double)a.eps + sqrt(vt_hat)));
+    a.m[id] = mt;
+    a.v[id] = vt;
+}
+
 struct Win1Args {
     const uint32_t *idx;
     const float *val;
@@ -343,6 +358,8 @@ struct Win1Args {
     uint32_t *dup;      // set by win_mark when an index repeats (or is >= n); zeroed by the last tile then
     bool fuse_sgd;      // ModuleCpuOptimize::run: optimize_raw on every winner as it is emitted
     SgdLaunch sgd;
+    bool fuse_adam;     // ... with Adam (no amsgrad)
+    AdamLaunch adam;
 };
 
 // WP pairs per lane: 4 (the default; 1,024-pair tiles, four times the
@@ -380,13 +397,21 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
                 v[b] = a.val[i];
             }
         }
-        float xp[WP], mp[WP];
+        float xp[WP], mp[WP], vp[WP];
         if (a.fuse_sgd) {  // every pair is a winner: its parameter and momentum words, loaded together
 #pragma unroll
             for (uint32_t b = 0; b < WP; ++b) {
                 const uint32_t id = e + b < a.m ? j[b] : 0u;
                 xp[b] = a.sgd.param[id];
                 mp[b] = a.sgd.mom ? a.sgd.mom[id] : 0.f;
+            }
+        } else if (a.fuse_adam) {
+#pragma unroll
+            for (uint32_t b = 0; b < WP; ++b) {
+                const uint32_t id = e + b < a.m ? j[b] : 0u;
+                xp[b] = a.adam.param[id];
+                mp[b] = a.adam.m[id];
+                vp[b] = a.adam.v[id];
             }
         }
 #pragma unroll
@@ -396,6 +421,7 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
                 a.out_idx[e + b] = j[b];
                 a.out_val[e + b] = g;
                 if (a.fuse_sgd) sgd_step(a.sgd, j[b], g, xp[b], mp[b]);  // indices unique: updates commute
+                else if (a.fuse_adam) adam_step(a.adam, j[b], g, xp[b], mp[b], vp[b]);
                 a.win[j[b]] = 0;  // scratch back to zero for the next call
             }
         }
@@ -423,13 +449,21 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
 #pragma unroll
         for (uint32_t b = 0; b < WP; ++b) v[b] = a.m ? a.val[std::min<size_t>(e + b, a.m - 1)] : 0.f;
     }
-    float xp[WP], mp[WP];
+    float xp[WP], mp[WP], vp[WP];
     if (a.fuse_sgd) {  // the winners' parameter and momentum words, loaded under the look-back
 #pragma unroll
         for (uint32_t b = 0; b < WP; ++b) {
             const uint32_t id = (keep >> b & 1u) ? j[b] : 0u;
             xp[b] = a.sgd.param[id];
             mp[b] = a.sgd.mom ? a.sgd.mom[id] : 0.f;
+        }
+    } else if (a.fuse_adam) {
+#pragma unroll
+        for (uint32_t b = 0; b < WP; ++b) {
+            const uint32_t id = (keep >> b & 1u) ? j[b] : 0u;
+            xp[b] = a.adam.param[id];
+            mp[b] = a.adam.m[id];
+            vp[b] = a.adam.v[id];
         }
     }
     uint32_t tc;
@@ -475,6 +509,7 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
                 a.out_val[P + r] = g;
             }
             if (a.fuse_sgd) sgd_step(a.sgd, j[b], g, xp[b], mp[b]);  // each index elected once: updates commute
+            else if (a.fuse_adam) adam_step(a.adam, j[b], g, xp[b], mp[b], vp[b]);
             a.win[j[b]] = 0;  // scratch back to zero for the next call
             ++r;
         }
@@ -573,11 +608,7 @@ __global__ void __launch_bounds__(STG_WG) adam_apply(AdamLaunch a) {
     const uint32_t stride = gridDim.x * STG_WG;
     for (uint32_t i = blockIdx.x * STG_WG + threadIdx.x; i < len; i += stride) {
         const uint32_t id = a.gidx[i];
-        const float x = a.param[id];
-        const AdamElem e = adam_elem(a, x, a.grad[i], id);
-        a.param[id] = (float)((double)x - e.num / ((double)a.eps + sqrt(e.vt_hat)));
-        a.m[id] = e.mt;
-        a.v[id] = e.vt;
+        adam_step(a, id, a.grad[i], a.param[id], a.m[id], a.v[id]);
     }
 }
 
@@ -735,7 +766,7 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
             const uint32_t nt1 = (uint32_t)((per_rank + wp * STG_WG - 1) / (wp * STG_WG));
             Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, 0ull /* win_mark zeroed it */, w1.tag,
                        out_idx, out_val, out_count, w1.fail, w1.dup, w1.sgd != nullptr,
-                       w1.sgd ? *w1.sgd : SgdLaunch{}};
+                       w1.sgd ? *w1.sgd : SgdLaunch{}, w1.adam != nullptr, w1.adam ? *w1.adam : AdamLaunch{}};
             if (wp == 16) win_emit1t<16><<<nt1, STG_WG, 0, s>>>(a);
             else if (wp == 2) win_emit1t<2><<<nt1, STG_WG, 0, s>>>(a);
             else if (wp == 1) win_emit1t<1><<<nt1, STG_WG, 0, s>>>(a);

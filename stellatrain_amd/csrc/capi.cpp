@@ -1127,15 +1127,11 @@ int stg_adam_destroy(stg_adam_t o) {
     return STG_OK;
 }
 
-int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param, uint32_t param_len,
-                                 const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
-                                 const uint32_t *d_grad_len, void *stream) {
-    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
-    if (o->amsgrad && grad_len > param_len)
-        return fail(STG_ERR_INVALID, "amsgrad: grad_len > param_len (indices must be unique)");
-    HIP_TRY(hipSetDevice(o->device));
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    stg::AdamLaunch a;
+// One optimize_raw call's launch arguments: the name's state (created zeroed
+// on its first call: adam.cpp:28-35), its tick and the bias corrections.
+static int adam_prepare(stg_adam_t o, const char *name, float *d_param, uint32_t param_len, hipStream_t s,
+                        stg::AdamLaunch *out) {
+    stg::AdamLaunch a{};
     uint32_t tick;
     {
         std::lock_guard<std::mutex> g(o->mu);
@@ -1169,10 +1165,6 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
     }
     a.param = d_param;
     a.param_len = param_len;
-    a.grad = d_grad;
-    a.gidx = d_idx;
-    a.grad_len = grad_len;
-    a.d_grad_len = d_grad_len;
     a.b1 = o->b1;
     a.b2 = o->b2;
     a.eps = o->eps;
@@ -1184,7 +1176,61 @@ int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param,
     a.maximize = o->maximize;
     a.tag = tick;
     a.fail = o->fail;
+    *out = a;
+    return STG_OK;
+}
+
+int stg_adam_optimize_raw_device(stg_adam_t o, const char *name, float *d_param, uint32_t param_len,
+                                 const float *d_grad, const uint32_t *d_idx, uint32_t grad_len,
+                                 const uint32_t *d_grad_len, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    if (o->amsgrad && grad_len > param_len)
+        return fail(STG_ERR_INVALID, "amsgrad: grad_len > param_len (indices must be unique)");
+    HIP_TRY(hipSetDevice(o->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    stg::AdamLaunch a;
+    int rc = adam_prepare(o, name, d_param, param_len, s, &a);
+    if (rc) return rc;
+    a.grad = d_grad;
+    a.gidx = d_idx;
+    a.grad_len = grad_len;
+    a.d_grad_len = d_grad_len;
     if (grad_len) HIP_TRY(stg::launch_adam(a, s));
+    return STG_OK;
+}
+
+int stg_merge_optimize_adam_device(stg_adam_t o, const char *name, float *d_param, uint32_t param_len,
+                                   const uint32_t *d_idx, const float *d_val, size_t per_rank, int world,
+                                   float *d_dense, uint8_t *d_mark, uint32_t *d_out_idx, float *d_out_val,
+                                   uint32_t *d_out_count, void *stream) {
+    if (!o || !name) return fail(STG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(o->device));
+    if (world != 1 || per_rank == 0 || o->amsgrad) {  // the merge, then the step over its output
+        int rc = stg_scatter_merge_device(d_idx, d_val, per_rank, world, param_len, d_dense, d_mark, d_out_idx,
+                                          d_out_val, d_out_count, stream);
+        if (rc) return rc;
+        const size_t cap = std::min<size_t>(per_rank * (size_t)world, o->amsgrad ? param_len : 0xffffffffu);
+        return stg_adam_optimize_raw_device(o, name, d_param, param_len, d_out_val, d_out_idx, (uint32_t)cap,
+                                            d_out_count, stream);
+    }
+    // world 1 without amsgrad: the step inside the emission (see the SGD form)
+    if (per_rank >= (size_t(1) << 32) || param_len == 0)
+        return fail(STG_ERR_UNSUPPORTED, "more than 2^32-1 elements or an empty parameter");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    stg::AdamLaunch a;
+    int rc = adam_prepare(o, name, d_param, param_len, s, &a);
+    if (rc) return rc;
+    int ncu = 256;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device));
+    MergeScratch *ms = merge_scratch(o->device, s);
+    std::lock_guard<std::mutex> g(ms->mu);
+    if ((rc = merge_scratch_ensure(ms, s, param_len, per_rank, world))) return rc;
+    if (++ms->tag == 0) ms->tag = 1;
+    uint32_t grid = 0;
+    stg::Win1Desc w1{ms->desc, ms->ticket, 0, ms->tag, &grid, ms->fail, reinterpret_cast<uint32_t *>(ms->ticket + 1)};
+    w1.adam = &a;
+    HIP_TRY(stg::launch_scatter_merge(d_idx, d_val, per_rank, world, param_len, d_dense, d_mark, d_out_idx, d_out_val,
+                                      d_out_count, ms->tiles, ms->win, ncu, s, w1));
     return STG_OK;
 }
 

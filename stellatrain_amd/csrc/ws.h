@@ -258,7 +258,8 @@ struct Win1Desc {
     uint32_t *grid_out;   // receives the tiles launched (the ticket advances by it)
     uint32_t *fail;       // sticky failure word of the scratch (a look-back that gave up)
     uint32_t *dup;        // world 1: set when an index repeats; the ticket then counts from 0 (win_mark zeroes it)
-    const struct SgdLaunch *sgd = nullptr;  // world 1: the SGD step fused into the emission (null: none)
+    const struct SgdLaunch *sgd = nullptr;    // world 1: the SGD step fused into the emission (null: none)
+    const struct AdamLaunch *adam = nullptr;  // ... or the Adam step (no amsgrad)
 };
 hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t per_rank, int world, size_t n,
                                 float *dense, uint8_t *mark, uint32_t *out_idx, float *out_val,

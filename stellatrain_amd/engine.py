@@ -258,6 +258,31 @@ def wire_decode(widx, wval, flag: int, idx=None, val=None):
     return idx, val
 
 
+def _merge_optimize(fn, h, param, name, idx, val, per_rank, world, dense, mark, out_idx, out_val, count):
+    """ModuleCpuOptimize::run through one C call (``fn``): the MERGE decompress
+    of ``world`` rank streams into the merged stream (returned), then the
+    optimizer's step on it."""
+    import torch
+    dev, n = param.device, param.numel()
+    if out_idx is None:
+        out_idx = torch.empty(per_rank * world, dtype=torch.int32, device=dev)
+    if out_val is None:
+        out_val = torch.empty(per_rank * world, dtype=torch.float32, device=dev)
+    if count is None:
+        count = torch.empty(1, dtype=torch.int32, device=dev)
+    if world > 1:
+        if dense is None:
+            dense = torch.zeros(n, dtype=torch.float32, device=dev)
+        if mark is None:
+            mark = torch.zeros(n, dtype=torch.uint8, device=dev)
+    dp = C.c_void_p(dense.data_ptr()) if dense is not None else None
+    mp = C.c_void_p(mark.data_ptr()) if mark is not None else None
+    check(fn(h, name.encode(), C.c_void_p(param.data_ptr()), n, C.c_void_p(idx.data_ptr()), C.c_void_p(val.data_ptr()),
+             per_rank, world, dp, mp, C.c_void_p(out_idx.data_ptr()), C.c_void_p(out_val.data_ptr()),
+             C.c_void_p(count.data_ptr()), C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+    return out_idx, out_val, count
+
+
 class SparseSGD:
     """``SGD`` sparse optimizer (optim/sgd.h:10-50) on the device.  Options as
     SGD::configure (sgd.cpp:265-300); ``optimize_raw`` as sgd.cpp:34-263."""
@@ -293,30 +318,10 @@ class SparseSGD:
     def merge_optimize(self, param, name: str, idx, val, per_rank: int, world: int = 1, dense=None, mark=None,
                        out_idx=None, out_val=None, count=None):
         """ModuleCpuOptimize::run (cpu_optimize.cpp:26-100): the MERGE
-        decompress of ``world`` rank streams of ``per_rank`` pairs into the
-        merged stream (returned, as ``scatter_merge``), then optimize_raw on it;
-        at world 1 the step runs inside the decompress's emission launch."""
-        import torch
-        dev, n = param.device, param.numel()
-        if out_idx is None:
-            out_idx = torch.empty(per_rank * world, dtype=torch.int32, device=dev)
-        if out_val is None:
-            out_val = torch.empty(per_rank * world, dtype=torch.float32, device=dev)
-        if count is None:
-            count = torch.empty(1, dtype=torch.int32, device=dev)
-        if world > 1:
-            if dense is None:
-                dense = torch.zeros(n, dtype=torch.float32, device=dev)
-            if mark is None:
-                mark = torch.zeros(n, dtype=torch.uint8, device=dev)
-        dp = C.c_void_p(dense.data_ptr()) if dense is not None else None
-        mp = C.c_void_p(mark.data_ptr()) if mark is not None else None
-        check(lib().stg_merge_optimize_sgd_device(
-            self._h, name.encode(), C.c_void_p(param.data_ptr()), n, C.c_void_p(idx.data_ptr()),
-            C.c_void_p(val.data_ptr()), per_rank, world, dp, mp, C.c_void_p(out_idx.data_ptr()),
-            C.c_void_p(out_val.data_ptr()), C.c_void_p(count.data_ptr()),
-            C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
-        return out_idx, out_val, count
+        decompress, then optimize_raw on its output; at world 1 the step runs
+        inside the decompress's emission launch."""
+        return _merge_optimize(lib().stg_merge_optimize_sgd_device, self._h, param, name, idx, val, per_rank, world,
+                               dense, mark, out_idx, out_val, count)
 
     def momentum_buffer(self, name: str, n: int):
         import torch
@@ -357,6 +362,13 @@ class SparseAdam:
             self._h, name.encode(), C.c_void_p(param.data_ptr()), param.numel(), C.c_void_p(grad.data_ptr()),
             C.c_void_p(gidx.data_ptr()), n, C.c_void_p(d_grad_len.data_ptr()) if d_grad_len is not None else None,
             C.c_void_p(torch.cuda.current_stream(param.device.index).cuda_stream)))
+
+    def merge_optimize(self, param, name: str, idx, val, per_rank: int, world: int = 1, dense=None, mark=None,
+                       out_idx=None, out_val=None, count=None):
+        """ModuleCpuOptimize::run with Adam: the step inside the decompress's
+        emission at world 1 without amsgrad, else the two calls."""
+        return _merge_optimize(lib().stg_merge_optimize_adam_device, self._h, param, name, idx, val, per_rank, world,
+                               dense, mark, out_idx, out_val, count)
 
     def check_device(self) -> None:
         """Raise if a device-side failure was flagged (amsgrad look-back timeout)."""

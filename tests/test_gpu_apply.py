@@ -280,6 +280,54 @@ def test_merge_optimize_sgd_world1_duplicates(gpu, oracle):
     oracle.sgd_free(hs)
 
 
+@pytest.mark.parametrize("amsgrad", [False, True])
+def test_merge_optimize_adam_world1(gpu, oracle, amsgrad):
+    """SparseAdam.merge_optimize at world 1 (the step in the emission launch;
+    amsgrad: the decompress, then the ordered step), duplicated and
+    duplicate-free streams alternating: parameters, m, v and vmax bit-exact
+    against the oracle's decompress + optimize_raw."""
+    import torch
+    from stellatrain_amd import SparseAdam
+    n, per_rank = 100013, 20000
+    opt = dict(lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, weight_decay=1e-4, amsgrad=amsgrad)
+    adam = SparseAdam(**opt)
+    ha = oracle.adam_new(**opt)
+    param0 = synth(n, seed_for(23, 96)) * np.float32(10)
+    po, pg = param0.copy(), torch.from_numpy(param0.copy()).to(gpu)
+    rng = np.random.default_rng(13)
+    for it, dups in enumerate([False, True, False, True]):
+        idx = rng.choice(n, per_rank, replace=False).astype(np.uint32)
+        if dups:
+            src = rng.integers(0, per_rank // 2, per_rank // 7)
+            idx[per_rank // 2:per_rank // 2 + src.size] = idx[src]
+        val = synth(per_rank, seed_for(63, it))
+        mi, mv = oracle.merge_decompress(idx, val, per_rank, 1, n)
+        oi, ov, cnt = adam.merge_optimize(pg, "a@weight", torch.from_numpy(idx.view(np.int32)).to(gpu),
+                                          torch.from_numpy(val).to(gpu), per_rank, 1)
+        m = int(cnt.item())
+        assert m == mi.size, (it, dups)
+        gi, gv = oi[:m].cpu().numpy().view(np.uint32), ov[:m].cpu().numpy()
+        ei, ev = _sorted_pairs(gi, gv)
+        xi, xv = _sorted_pairs(mi.astype(np.uint32), mv)
+        assert np.array_equal(ei, xi) and np.array_equal(ev.view(np.uint32), xv.view(np.uint32)), (it, dups)
+        # amsgrad's running maximum follows the stream's order, which the
+        # reference leaves to unordered_set (cpu_optimize.cpp:14-24): the step is
+        # checked on the merged stream in the order it was emitted
+        if amsgrad:
+            oracle.adam_apply(ha, "a@weight", po, gv, gi)
+        else:
+            oracle.adam_apply(ha, "a@weight", po, mv, mi)
+        assert np.array_equal(pg.cpu().numpy().view(np.uint32), po.view(np.uint32)), (it, dups)
+    adam.check_device()
+    mo, vo, vmo, _ = oracle.adam_state(ha, "a@weight", n)
+    mg, vg, vmg, _ = adam.state("a@weight", n)
+    assert np.array_equal(mg.view(np.uint32), mo.view(np.uint32))
+    assert np.array_equal(vg.view(np.uint32), vo.view(np.uint32))
+    if amsgrad:
+        assert np.float32(vmg).view(np.uint32) == np.float32(vmo).view(np.uint32)
+    oracle.adam_free(ha)
+
+
 def test_error_feedback_residual(gpu, oracle):
     """compress.cpp:172-186: after compress, src[idx[i]] = 0 for every slot
     i < numel and the bucket is copied into the residual."""

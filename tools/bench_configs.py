@@ -264,8 +264,8 @@ def c5_round_trip(torch, steps, kind="sgd"):
     for i, p in enumerate(params):
         fill(lib(), p, 777 + i, st.cuda_stream)
     comp = ThresholdvCompressor16()
-    fused = kind == "sgd_fused"
-    sgd, label = make_opt("sgd" if fused else kind)
+    fused = kind.endswith("_fused")
+    sgd, label = make_opt(kind[:-len("_fused")] if fused else kind)
     if fused:
         label += ", one merge_optimize call (step fused into the decompress)"
     idx = torch.zeros(k, dtype=torch.int32, device=dev)
@@ -561,7 +561,7 @@ def main():
     if "single" in only:  # one 64 MiB bucket per call, one stream: the latency of a lone call
         emit(time_device(torch, make_compressor("thresholdv16"), "thresholdv16 single-bucket", 64, 0.99, a.calls, 8, 16))
     if "c5" in only:
-        for kind in ("sgd", "sgd_fused", "adam", "adam_ams"):
+        for kind in ("sgd", "sgd_fused", "adam", "adam_fused", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))
     if "gather" in only:
         for d in gather(torch, a.calls):
