@@ -311,6 +311,150 @@ __device__ void adjust_heap(uint2 *H, uint32_t hole, uint32_t len, uint2 value) 
     hst(H, hole, value);
 }
 
+// The pops of the literal heap, by one wave.  Each pop is GCC's pop_heap /
+// __adjust_heap / __push_heap exactly (the element moves are the same); only
+// where the nodes are read differs:
+//  * positions < HC (depths 0..12) are held in LDS (Hl);
+//  * the descent reads its nodes a batch at a time: every node of the next
+//    4 or 8 levels below the hole in one round of loads (batch roots at depths
+//    0, 4, 12, 20, ...), then walks those levels with readlane.  The depths
+//    13..20 of a 2^20-line bucket are one round of global loads per pop
+//    instead of eight dependent ones.
+//  * every global position p is loaded and stored only by lane hl_lane(p)
+//    (its lane in the one batch that holds its depth), so a lane re-reads what
+//    it wrote itself;
+//  * __push_heap climbs the descent path, whose new contents are kept in pv.
+constexpr uint32_t HC = 8191;  // heap positions held in LDS by the pops
+static_assert(sizeof(uint2) * (HC + 32) <= sizeof(decltype(FillLds::u)), "the LDS heap fits the union");
+__device__ __forceinline__ uint32_t hl_rootdepth(uint32_t dd) { return dd <= 4 ? 0u : 4u + ((dd - 5u) >> 3) * 8u; }
+__device__ __forceinline__ uint32_t hl_lane(uint32_t p) {
+    const uint32_t dd = depth_of(p + 1), j = dd - hl_rootdepth(dd);
+    return (p + 1) & ((1u << min(j, 6u)) - 1u);
+}
+__device__ __forceinline__ uint2 rl2(uint2 v, uint32_t l) {
+    return make_uint2(__builtin_amdgcn_readlane(v.x, l), __builtin_amdgcn_readlane(v.y, l));
+}
+__device__ __forceinline__ void hl_put(uint2 *Hl, uint2 *H, uint32_t p, uint2 v, uint32_t lane) {
+    if (p < HC) Hl[p] = v;  // every lane writes the same value
+    else if (lane == hl_lane(p)) hst(H, p, v);
+}
+// level j (1..8) of a batch: offset o in slot (j <= 6 ? j - 1 : j == 7 ? 6 + o / 64 : 8 + o / 64), lane o % 64.
+// A batch is all in LDS (roots at depths 0, 4) or all in global memory (roots
+// at depths 12, 20, ...).  The loads carry no branches (a node past the heap
+// reads a clamped LDS slot or 0 from the bounded buffer and is never walked
+// to), so a batch's loads are all in flight together.
+__device__ __forceinline__ uint2 hb_gld(__amdgpu_buffer_rsrc_t r, uint64_t p, uint32_t L) {
+    typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+    const uint32_t off = p < L ? (uint32_t)p * 8u : 0xfffffff0u;
+    const u2v v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16 /* sc1 */);
+    return make_uint2(v.x, v.y);
+}
+template <int D, bool GLB>
+__device__ __forceinline__ void hb_load(uint2 (&b)[12], const uint2 *Hl, __amdgpu_buffer_rsrc_t r, uint32_t root,
+                                        uint32_t L, uint32_t lane) {
+#pragma unroll
+    for (int j = 1; j <= D; ++j) {
+        const int ns = j <= 6 ? 1 : (1 << (j - 6)), s0 = j <= 6 ? j - 1 : (j == 7 ? 6 : 8);
+#pragma unroll
+        for (int q = 0; q < ns; ++q) {
+            const uint64_t p = (((uint64_t)root + 1) << j) - 1 + (uint32_t)q * 64u + lane;
+            b[s0 + q] = GLB ? hb_gld(r, p, L) : Hl[min(p, (uint64_t)HC - 1)];
+        }
+    }
+}
+template <int J>
+__device__ __forceinline__ uint2 hb_node(const uint2 (&b)[12], uint32_t o) {
+    if constexpr (J <= 6) return rl2(b[J - 1], o);
+    else if constexpr (J == 7) return (o >> 6) ? rl2(b[7], o & 63u) : rl2(b[6], o & 63u);
+    const uint32_t g = o >> 6, l = o & 63u;
+    const uint2 a0 = rl2(b[8], l), a1 = rl2(b[9], l), a2 = rl2(b[10], l), a3 = rl2(b[11], l);
+    return g == 0 ? a0 : g == 1 ? a1 : g == 2 ? a2 : a3;
+}
+// Level J of the walk below a batch root (the hole at offset o of level J - 1).
+// Returns false when the descent has ended.
+template <int J, int D>
+__device__ __forceinline__ bool hb_steps(const uint2 (&b)[12], uint2 *Hl, uint2 *H, uint2 *pv, uint32_t &hole,
+                                         uint32_t o, uint32_t L, uint32_t lane) {
+    if constexpr (J > D) {
+        return true;
+    } else {
+        const uint32_t dh = depth_of(hole + 1);
+        if (hole < (L - 1) / 2) {
+            const uint2 cl = hb_node<J>(b, 2 * o), cr = hb_node<J>(b, 2 * o + 1);
+            const bool left = u2f(cr.x) < u2f(cl.x);
+            const uint2 c = left ? cl : cr;
+            hl_put(Hl, H, hole, c, lane);
+            pv[dh] = c;
+            hole = 2 * hole + (left ? 1u : 2u);
+            return hb_steps<J + 1, D>(b, Hl, H, pv, hole, 2 * o + (left ? 0u : 1u), L, lane);
+        }
+        if ((L & 1u) == 0 && hole == (L - 2) / 2) {  // a left child only
+            const uint2 c = hb_node<J>(b, 2 * o);
+            hl_put(Hl, H, hole, c, lane);
+            pv[dh] = c;
+            hole = 2 * hole + 1;
+        }
+        return false;
+    }
+}
+// Walk up to D levels below `hole` (a batch root) for a heap of length L.
+template <int D, bool GLB>
+__device__ __forceinline__ bool hb_walk(uint2 *Hl, uint2 *H, __amdgpu_buffer_rsrc_t r, uint2 *pv, uint32_t &hole,
+                                        uint32_t L, uint32_t lane) {
+    uint2 b[12];
+    hb_load<D, GLB>(b, Hl, r, hole, L, lane);
+    return hb_steps<1, D>(b, Hl, H, pv, hole, 0u, L, lane);
+}
+template <typename T>
+__device__ __forceinline__ T *uni_ptr(T *p) {  // a wave-uniform pointer, in SGPRs
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    return reinterpret_cast<T *>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a));
+}
+// (noinline: the kernel keeps its own register budget; the arguments are
+// made wave-uniform again here, so the walk's branches and readlanes are scalar)
+__device__ __attribute__((noinline)) uint32_t wave_pops(uint2 *Hl, uint2 *pv, uint2 *H, uint32_t N, uint32_t rem,
+                                                        uint32_t end, uint32_t lane) {
+    Hl = uni_ptr(Hl);
+    pv = uni_ptr(pv);
+    H = uni_ptr(H);
+    N = __builtin_amdgcn_readfirstlane(N);
+    rem = __builtin_amdgcn_readfirstlane(rem);
+    end = __builtin_amdgcn_readfirstlane(end);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(H, 0, N * 8u, 0x00020000);
+    uint32_t len = N, acc = 0, np = 0;
+    while (acc < rem && len > 0) {
+        const uint2 top = Hl[0];
+        const uint32_t n_el = min(16u, min(end - top.y, rem - acc));
+        acc += n_el;
+        ++np;
+        if (len > 1) {
+            const uint32_t L = len - 1, lv = hl_lane(L);
+            // the last element: its global load is read only at the climb
+            const uint2 vl = Hl[min(L, HC - 1)], vg = hb_gld(r, L, L + 1);
+            hl_put(Hl, H, L, top, lane);
+            // __adjust_heap(first, 0, L, v): batches at depths 0 (4 levels), 4 (8), 12, 20, ... (8)
+            uint32_t hole = 0;
+            if (hb_walk<4, false>(Hl, H, r, pv, hole, L, lane) && hb_walk<8, false>(Hl, H, r, pv, hole, L, lane))
+                while (hb_walk<8, true>(Hl, H, r, pv, hole, L, lane)) {
+                }
+            // __push_heap: the path above the hole holds pv[0 .. depth - 1]
+            const uint2 v = L < HC ? vl : rl2(vg, lv);
+            uint32_t dh = depth_of(hole + 1);
+            while (hole > 0) {
+                const uint2 pc = pv[dh - 1];
+                if (!(u2f(pc.x) < u2f(v.x))) break;
+                hl_put(Hl, H, hole, pc, lane);
+                hole = (hole - 1) / 2;
+                --dh;
+            }
+            hl_put(Hl, H, hole, v, lane);
+        }
+        --len;
+    }
+    return np;
+}
+
 __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uint32_t N, float t, bool tail,
                           float tail_key, uint32_t *fail) {
     uint2 *H = d.heap;
@@ -350,25 +494,20 @@ __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uin
             __syncthreads();
         }
     }
-    // pops (one lane): pop_heap moves the top to the end, so the popped
-    // candidates end up at H[N-1], H[N-2], ...
+    // pops (wave 0): pop_heap moves the top to the end, so the popped
+    // candidates end up at H[N-1], H[N-2], ...  The top HC positions live in
+    // LDS meanwhile (written back below).
     const uint32_t rem = d.dst_len - cnt;
-    if (tid == 0) {
-        uint32_t len = N, acc = 0, np = 0;
-        while (acc < rem && len > 0) {
-            const uint2 top = hld(H, 0);
-            const uint32_t n_el = min(16u, min(d.nb * 16 + d.tl - top.y, rem - acc));
-            acc += n_el;
-            ++np;
-            if (len > 1) {
-                const uint2 v = hld(H, len - 1);
-                hst(H, len - 1, top);
-                adjust_heap(H, 0, len - 1, v);
-            }
-            --len;
-        }
-        S.npop = np;
+    uint2 *Hl = reinterpret_cast<uint2 *>(&S.u);
+    const uint32_t nl = min(N, HC);
+    for (uint32_t p = tid; p < nl; p += FILL_WG) Hl[p] = hld(H, p);
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t np = wave_pops(Hl, Hl + HC, H, N, rem, d.nb * 16 + d.tl, tid);
+        if (tid == 0) S.npop = np;
     }
+    __syncthreads();
+    for (uint32_t p = tid; p < nl; p += FILL_WG) hst(H, p, Hl[p]);
     vm_drain();
     __syncthreads();
     const uint32_t np = S.npop;
