@@ -354,7 +354,7 @@ struct Win1Args {
     uint32_t *out_idx;
     float *out_val;
     uint32_t *out_count;
-    uint32_t *fail;     // sticky failure word: a tile whose look-back gave up
+    uint32_t *fail;     // [0] sticky failure bits (a tile whose look-back gave up); [1] the tag of the last call that did
     uint32_t *dup;      // set by win_mark when an index repeats (or is >= n); zeroed by the last tile then
     bool fuse_sgd;      // ModuleCpuOptimize::run: optimize_raw on every winner as it is emitted
     SgdLaunch sgd;
@@ -427,7 +427,7 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
         }
         if (tid == 0 && blockIdx.x == a.ntiles - 1) {
             __builtin_amdgcn_s_waitcnt(0);
-            *a.out_count = ld_sc1(a.fail) ? 0xffffffffu : (uint32_t)a.m;
+            *a.out_count = (uint32_t)a.m;  // no look-back in this call: nothing of it can have failed
         }
         return;
     }
@@ -499,7 +499,10 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     // scratch's sticky failure word (stg_scatter_merge_check) and, as the last
     // tile, poisons the count; the last tile also poisons it for any earlier
     // tile that gave up first
-    if (bad && tid == 0) g_or(a.fail, FAIL_SPIN_TIMEOUT);
+    if (bad && tid == 0) {
+        g_or(a.fail, FAIL_SPIN_TIMEOUT);  // sticky, for stg_scatter_merge_check
+        st_sc1(a.fail + 1, a.tag);        // this call's count is poisoned, later calls' are not
+    }
 #pragma unroll
     for (uint32_t b = 0; b < WP; ++b) {
         if (keep >> b & 1u) {
@@ -516,19 +519,27 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
     }
     if (tid == 0 && tile == a.ntiles - 1) {
         __builtin_amdgcn_s_waitcnt(0);
-        *a.out_count = (bad || ld_sc1(a.fail)) ? 0xffffffffu : (uint32_t)(P + tc);
+        *a.out_count = (bad || ld_sc1(a.fail + 1) == a.tag) ? 0xffffffffu : (uint32_t)(P + tc);
         // every tile read the flag before publishing its count (the look-back
         // above saw them all): clear it for the next call
         if (!bad) st_sc1(a.dup, 0u);
     }
 }
 
+// a device count of POISON_COUNT (a failed producer) is length 0: never step
+// over slots nobody wrote
+__device__ __forceinline__ uint32_t dev_len(uint32_t cap, const uint32_t *d_len) {
+    if (!d_len) return cap;
+    const uint32_t c = *d_len;
+    return c == POISON_COUNT ? 0u : min(cap, c);
+}
+
 __global__ void __launch_bounds__(STG_WG) sgd_apply(SgdLaunch a) {
-    uint32_t len = a.grad_len;
-    if (a.d_grad_len) len = min(len, *a.d_grad_len);
+    const uint32_t len = dev_len(a.grad_len, a.d_grad_len);
     const uint32_t stride = gridDim.x * STG_WG;
     for (uint32_t i = blockIdx.x * STG_WG + threadIdx.x; i < len; i += stride) {
         const uint32_t id = a.gidx[i];
+        if (id >= a.param_len) continue;  // an index past the parameter (bad input): never written
         const float x = a.param[id];
         float g = a.grad[i];
         if (a.weight_decay != 0.f) g = fmaf(a.weight_decay, x, g);
@@ -599,15 +610,14 @@ __device__ __forceinline__ AdamElem adam_elem(const AdamLaunch &a, float x, floa
     return e;
 }
 
-__device__ __forceinline__ uint32_t adam_len(const AdamLaunch &a) {
-    return a.d_grad_len ? min(a.grad_len, *a.d_grad_len) : a.grad_len;
-}
+__device__ __forceinline__ uint32_t adam_len(const AdamLaunch &a) { return dev_len(a.grad_len, a.d_grad_len); }
 
 __global__ void __launch_bounds__(STG_WG) adam_apply(AdamLaunch a) {
     const uint32_t len = adam_len(a);
     const uint32_t stride = gridDim.x * STG_WG;
     for (uint32_t i = blockIdx.x * STG_WG + threadIdx.x; i < len; i += stride) {
         const uint32_t id = a.gidx[i];
+        if (id >= a.param_len) continue;  // an index past the parameter (bad input): never written
         adam_step(a, id, a.grad[i], a.param[id], a.m[id], a.v[id]);
     }
 }
@@ -659,7 +669,7 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
         id[j] = 0;
         x[j] = 0.f;
         e[j] = AdamElem{0.f, 0.f, 0.0, 0.0};
-        if (i < len) {
+        if (i < len && a.gidx[i] < a.param_len) {  // an index past the parameter (bad input): skipped
             id[j] = a.gidx[i];
             x[j] = a.param[id[j]];
             e[j] = adam_elem(a, x[j], a.grad[i], id[j]);
@@ -706,7 +716,7 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
     for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t i = base + j;
         pre = max(pre, key[j]);
-        if (i < len) {
+        if (i < len && a.gidx[i] < a.param_len) {
             const float vm = ams_unkey(pre);
             a.param[id[j]] = (float)((double)x[j] - e[j].num / (double)(sqrtf(vm) + a.eps));
             a.m[id[j]] = e[j].mt;

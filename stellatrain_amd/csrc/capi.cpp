@@ -56,6 +56,7 @@ struct Workspace {
     void *fixed = nullptr;
     size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0, cap_desc = 0, cap_lone = 0;
     uint32_t epoch = 0;  // thresholdv16 call counter (hand-off tags)
+    uint32_t tk_tag = 0; // one-launch top-k call counter (topk1.hip)
     // threshold-v: the ticket's value at the next call, the last call's
     // range-descriptor tag and the descriptor block last zeroed (tile_cnt, its size)
     uint64_t tv_base = 0;
@@ -108,6 +109,9 @@ struct Workspace {
         const size_t o_tvt = carve(sizeof(uint64_t));
         const size_t o_wh = carve(sizeof(uint32_t) * stg::LNBIN);
         const size_t o_we = carve(sizeof(uint2) * stg::LNBIN * stg::LBCAP);
+        const size_t o_crew = carve(sizeof(stg::CrewCtl) * stg::MAX_BATCH);
+        const size_t o_tkc = carve(sizeof(stg::TopkCtl) * 2);
+        const size_t o_tkf = carve(sizeof(uint32_t) * stg::TK1_FINE);
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
         // control block are ordered after it (a plain hipMemset runs on the
@@ -123,6 +127,9 @@ struct Workspace {
         d.tv_ticket = reinterpret_cast<uint64_t *>(b + o_tvt);
         d.whist = reinterpret_cast<uint32_t *>(b + o_wh);
         d.went = reinterpret_cast<uint2 *>(b + o_we);
+        d.crew = reinterpret_cast<stg::CrewCtl *>(b + o_crew);
+        d.tkctl = reinterpret_cast<stg::TopkCtl *>(b + o_tkc);
+        d.tkfine = reinterpret_cast<uint32_t *>(b + o_tkf);
         return STG_OK;
     }
 
@@ -419,7 +426,7 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     // simply interleave as slots free up (STG_TV16_SHARE=1 splits the slots
     // evenly between the in-flight launches instead).
     static const bool share = getenv("STG_TV16_SHARE") && atoi(getenv("STG_TV16_SHARE")) == 1;
-    a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / std::max(inflight, 4u) * XCDS)
+    a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / (inflight ? inflight : 4u) * XCDS)
                      : (uint32_t)(2 * h->num_cu);
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     a.lone_cap = (uint32_t)ws->cap_lone;
@@ -510,6 +517,13 @@ int ef_after(stg_codec *h, const stg_bucket_t &b, float *resid, bool fused, hipS
     return STG_OK;
 }
 
+// Top-k in one launch steered by the key's last k-th magnitude (topk1.hip);
+// STG_TOPK_ONE=0: the select's launches (topk.hip) every call
+bool topk_one_launch() {
+    static const bool v = !(getenv("STG_TOPK_ONE") && atoi(getenv("STG_TOPK_ONE")) == 0);
+    return v;
+}
+
 int run_device(stg_codec *h, const char *key, const float *d_src, const void *key_ptr, size_t n, uint32_t k,
                uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset, uint32_t *d_count,
                hipStream_t s) {
@@ -558,7 +572,17 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         if ((rc = ws->ensure(2 * ntiles * stg::TOPK_SUP_CAP + 2 * stg::TOPK_LIST_CAP, 3 * ntiles + 1, 1))) return rc;
         stg::TopkLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, h->method == M_TOPK, d_count,
                           h->num_cu, ev};
-        HIP_TRY(stg::launch_topk(a, ws->d, s));
+        const size_t m = h->method == M_TOPK ? (n + 3) / 4 : n;
+        if (topk_one_launch() && (m + stg::TV_TILE - 1) / stg::TV_TILE <= stg::TOPK_LIST_TILES) {
+            // one launch, steered by the key's last k-th magnitude (its first call: the select inside it)
+            KeyState *st;
+            bool fresh;
+            if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
+            if (++ws->tk_tag == 0) ws->tk_tag = 1;
+            HIP_TRY(stg::launch_topk1(a, ws->d, st, !fresh, ws->tk_tag, s));
+        } else {
+            HIP_TRY(stg::launch_topk(a, ws->d, s));
+        }
     }
     return STG_OK;
 }
@@ -587,13 +611,15 @@ struct MergeScratch {
     }
 };
 std::mutex g_merge_mu;
-std::map<std::pair<int, hipStream_t>, std::unique_ptr<MergeScratch>> g_merge;
+// shared: a caller holds its reference for the whole call, so a concurrent
+// stg_scatter_merge_release never frees a scratch another thread has looked up
+std::map<std::pair<int, hipStream_t>, std::shared_ptr<MergeScratch>> g_merge;
 
-MergeScratch *merge_scratch(int dev, hipStream_t s) {
+std::shared_ptr<MergeScratch> merge_scratch(int dev, hipStream_t s) {
     std::lock_guard<std::mutex> g(g_merge_mu);
     auto &slot = g_merge[{dev, s}];
-    if (!slot) { slot = std::make_unique<MergeScratch>(); slot->device = dev; }
-    return slot.get();
+    if (!slot) { slot = std::make_shared<MergeScratch>(); slot->device = dev; }
+    return slot;
 }
 
 // Caller holds m->mu.
@@ -617,9 +643,9 @@ int merge_scratch_ensure(MergeScratch *m, hipStream_t s, size_t n, size_t per_ra
         HIP_TRY(hipMalloc(&m->ticket, 2 * sizeof(uint64_t)));
         HIP_TRY(hipMemsetAsync(m->ticket, 0, 2 * sizeof(uint64_t), s));
     }
-    if (!m->fail) {
-        HIP_TRY(hipMalloc(&m->fail, sizeof(uint32_t)));
-        HIP_TRY(hipMemsetAsync(m->fail, 0, sizeof(uint32_t), s));
+    if (!m->fail) {  // [0] sticky failure bits, [1] the tag of the last call that failed
+        HIP_TRY(hipMalloc(&m->fail, 2 * sizeof(uint32_t)));
+        HIP_TRY(hipMemsetAsync(m->fail, 0, 2 * sizeof(uint32_t), s));
     }
     const size_t words = std::max<size_t>(world > 1 ? 2 * n : n, 1);  // world > 1: two election halves
     if (words > m->cap_win) {
@@ -924,9 +950,9 @@ int stg_scatter_merge_device(const uint32_t *d_idx, const float *d_val, size_t p
     int ncu = 256;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    MergeScratch *ms = merge_scratch(dev, s);
+    const std::shared_ptr<MergeScratch> ms = merge_scratch(dev, s);
     std::lock_guard<std::mutex> g(ms->mu);
-    int rc = merge_scratch_ensure(ms, s, n, per_rank, world);
+    int rc = merge_scratch_ensure(ms.get(), s, n, per_rank, world);
     if (rc) return rc;
     if (++ms->tag == 0) ms->tag = 1;
     uint32_t grid = 0;
@@ -941,12 +967,12 @@ int stg_scatter_merge_check(void *stream) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    MergeScratch *ms = nullptr;
+    std::shared_ptr<MergeScratch> ms;
     {
         std::lock_guard<std::mutex> g(g_merge_mu);
         auto it = g_merge.find({dev, s});
         if (it == g_merge.end()) return STG_OK;  // no merge on this stream yet
-        ms = it->second.get();
+        ms = it->second;
     }
     std::lock_guard<std::mutex> g(ms->mu);
     HIP_TRY(hipStreamSynchronize(s));
@@ -964,7 +990,7 @@ int stg_scatter_merge_release(void *stream) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    std::unique_ptr<MergeScratch> ms;
+    std::shared_ptr<MergeScratch> ms;
     {
         std::lock_guard<std::mutex> g(g_merge_mu);
         auto it = g_merge.find({dev, s});
@@ -973,10 +999,10 @@ int stg_scatter_merge_release(void *stream) {
         g_merge.erase(it);
     }
     {
-        std::lock_guard<std::mutex> g(ms->mu);  // no call of another thread still inside
+        std::lock_guard<std::mutex> g(ms->mu);  // calls already inside finish first
         HIP_TRY(hipStreamSynchronize(s));
     }
-    ms.reset();
+    ms.reset();  // freed here, or by the last caller still holding it
     return STG_OK;
 }
 
@@ -1077,9 +1103,9 @@ int stg_merge_optimize_sgd_device(stg_sgd_t o, const char *name, float *d_param,
     if (rc) return rc;
     int ncu = 256;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device));
-    MergeScratch *ms = merge_scratch(o->device, s);
+    const std::shared_ptr<MergeScratch> ms = merge_scratch(o->device, s);
     std::lock_guard<std::mutex> g(ms->mu);
-    if ((rc = merge_scratch_ensure(ms, s, param_len, per_rank, world))) return rc;
+    if ((rc = merge_scratch_ensure(ms.get(), s, param_len, per_rank, world))) return rc;
     if (++ms->tag == 0) ms->tag = 1;
     uint32_t grid = 0;
     stg::Win1Desc w1{ms->desc, ms->ticket, 0, ms->tag, &grid, ms->fail, reinterpret_cast<uint32_t *>(ms->ticket + 1)};
@@ -1222,9 +1248,9 @@ int stg_merge_optimize_adam_device(stg_adam_t o, const char *name, float *d_para
     if (rc) return rc;
     int ncu = 256;
     HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, o->device));
-    MergeScratch *ms = merge_scratch(o->device, s);
+    const std::shared_ptr<MergeScratch> ms = merge_scratch(o->device, s);
     std::lock_guard<std::mutex> g(ms->mu);
-    if ((rc = merge_scratch_ensure(ms, s, param_len, per_rank, world))) return rc;
+    if ((rc = merge_scratch_ensure(ms.get(), s, param_len, per_rank, world))) return rc;
     if (++ms->tag == 0) ms->tag = 1;
     uint32_t grid = 0;
     stg::Win1Desc w1{ms->desc, ms->ticket, 0, ms->tag, &grid, ms->fail, reinterpret_cast<uint32_t *>(ms->ticket + 1)};

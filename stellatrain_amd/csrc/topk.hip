@@ -541,11 +541,16 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
             a.val[s] = 0.f;
         }
     }
-    // the count, unless a tile already found the select inconsistent (one
-    // finding it later poisons the count itself)
+    // the count, then the failure word again: a tile whose select_broken (fail
+    // bit, then POISON_COUNT) came before that second read is seen there and
+    // poisoned here; one that came after it stores its poison after ours
     if (tile == 0 && tid == 0) {
         __builtin_amdgcn_s_waitcnt(0);
-        if (!(ld_sc1(a.fail) & FAIL_SELECT)) st_sc1(a.count_out, a.cap);
+        if (!(ld_sc1(a.fail) & FAIL_SELECT)) {
+            st_sc1(a.count_out, a.cap);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (ld_sc1(a.fail) & FAIL_SELECT) st_sc1(a.count_out, POISON_COUNT);
+        }
     }
 }
 

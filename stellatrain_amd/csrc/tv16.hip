@@ -726,6 +726,18 @@ tv16_batch(BatchArgs A) {
     }
 }
 
+// Workgroups of a fill launch that order window-miss buckets (tv16wide.h): they
+// exit at once when no bucket of the launch needs them.
+uint32_t crew_batch() {
+    static const uint32_t v = getenv("STG_TV16_CREW") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW"))) : 64u;
+    return v ? std::min(std::max(v, MAX_BATCH + 1u), 1024u) : 0u;  // > MAX_BATCH: see tv16wide.h crew_loop
+}
+uint32_t crew_lone() {
+    static const uint32_t v =
+        getenv("STG_TV16_CREW_LONE") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW_LONE"))) : 128u;
+    return v ? std::min(std::max(v, MAX_BATCH + 1u), 1024u) : 0u;
+}
+
 }  // namespace
 
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
@@ -843,6 +855,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.state = a.b[0].state;
         F.cp = ws.cp;
         F.resid = a.b[0].resid;
+        F.crew = crew_lone();
+        F.crew_ctl = ws.crew;
         if ((e = launch_tv16_fill(F, s)) != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[2], s);
         return hipGetLastError();
@@ -877,6 +891,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
         F.helpers = F.lone ? std::min(helpers, 63u) : 0u;
         F.cc = &ws.ctl->cc[a.epoch & 1u];
+        F.crew = F.lone ? crew_lone() : crew_batch();
+        F.crew_ctl = ws.crew;
         const hipError_t e = launch_tv16_fill(F, s);
         if (e != hipSuccess) return e;
     }

@@ -210,7 +210,7 @@ __device__ __forceinline__ uint32_t rf_key(uint32_t pos) {
 // lanes per line (a float4 each: one 64-byte request per line), eight rounds
 // of loads in flight before their stores.
 template <uint32_t K = 5, typename GetPos>
-__device__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np, uint32_t tail_rank,
+__device__ __forceinline__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np, uint32_t tail_rank,
                            GetPos pos_of, uint32_t i_lo = 0, uint32_t i_hi = 0xffffffffu) {
     np = min(np, i_hi);  // ranks [i_lo, min(np, i_hi)) of the order
     constexpr uint32_t LPR = FILL_WG / 4;  // lines per round; K rounds of loads in flight
@@ -455,10 +455,13 @@ __device__ __attribute__((noinline)) uint32_t wave_pops(uint2 *Hl, uint2 *pv, ui
     return np;
 }
 
-__device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uint32_t N, float t, bool tail,
+__device__ void full_path(FillLds &S, const Tv16FillBucket d, uint32_t cnt, uint32_t N, float t, bool tail,
                           float tail_key, uint32_t *fail) {
     uint2 *H = d.heap;
     const uint32_t tid = threadIdx.x;
+    __syncthreads();
+    if (tid == 0) { S.flag = NONE; S.npop = 0; }  // the tail's rank below starts from NONE (any caller)
+    __syncthreads();
     // the candidate vector: every line with !(S >= t) in scan order, then the tail
     uint32_t base = 0;
     for (uint32_t l0 = 0; l0 < d.nb; l0 += FILL_WG) {
@@ -520,6 +523,7 @@ __device__ void full_path(FillLds &S, const Tv16FillBucket &d, uint32_t cnt, uin
 }
 
 #include "tv16lfin.h"
+#include "tv16wide.h"
 
 // Registers for 8 waves per SIMD (<= 64 VGPRs): the workgroup's two waves per
 // SIMD run beside the six of two scan workgroups.  The LDS is dynamic: the
@@ -538,11 +542,19 @@ tv16_fill(Tv16FillArgs A) {
     // emit a share of it (each waits only on a workgroup already running)
     __shared__ uint32_t s_role, s_last;
     const uint32_t tid = threadIdx.x;
+    if (!LONE && blockIdx.x >= A.nbk) {  // the crew (tv16wide.h)
+        crew_from_decisions(*reinterpret_cast<WideLds *>(fill_lds), S, A);
+        return;
+    }
     uint32_t role = 0;
-    if (LONE && (A.helpers || A.lfin)) {
+    if (LONE && (A.helpers || A.lfin || A.crew)) {
         if (tid == 0) s_role = g_add(&A.cc->pad[0], 1u);
         __syncthreads();
         role = s_role;
+    }
+    if (LONE && !A.lfin && role > A.helpers) {  // the crew of a lone launch with helpers
+        crew_from_decisions(*reinterpret_cast<WideLds *>(fill_lds), S, A);
+        return;
     }
     // lfin (tv16lfin.h): tickets [0, workers) finish the scan, the next
     // `rankers` order the regime-B fill in parallel; the last workgroup to
@@ -576,6 +588,10 @@ tv16_fill(Tv16FillArgs A) {
         __syncthreads();
         if (role < A.workers) lfin_worker(Lf, role);
         else if (role < A.workers + A.rankers) lfin_ranker(Lf, role - A.workers);
+        else {  // the crew (tv16wide.h): not counted among the roles below
+            crew_lfin(Lf, A);
+            return;
+        }
         vm_drain();  // every wave's stores drained, then one add for the workgroup
         __syncthreads();
         if (tid == 0) s_last = g_add(&A.cc->pad[4], 1u) == A.workers + A.rankers - 1;
@@ -631,8 +647,8 @@ tv16_fill(Tv16FillArgs A) {
         }
         const uint64_t h1 = ld_sc1(&D.w[1]);
         if ((uint32_t)(h0 >> 32) != ((A.epoch << 8) | TV16_TAG_DEC) || !((uint32_t)h0 & TV16_DEC_B) ||
-            ld_sc1(A.fail) || share > A.helpers)
-            return;  // no regime-B fill (or the scan failed): nothing to emit
+            ld_sc1(A.fail) || share > A.helpers || (A.crew && crew_wants((uint32_t)h0, (uint32_t)h1, A.mode)))
+            return;  // no regime-B fill (or the scan failed, or the crew orders it): nothing to emit
         if (!(uint32_t)h1 && !((uint32_t)h0 & TV16_DEC_TAIL)) return;  // nothing missing (the orderer returns too)
         uint64_t st0 = 0;
         for (uint32_t spins = 0; ld_sc1(&A.cc->pad[1]) != ready_tag; ++spins) {
@@ -708,12 +724,14 @@ tv16_fill(Tv16FillArgs A) {
     const uint32_t N = d.nb - Qtot + (tail ? 1u : 0u);  // candidate vector length
     const uint32_t rem = d.dst_len - cnt;
     if (!M && !tail) return;
+    if (A.crew && crew_wants(flags, M, A.mode)) return;  // a window miss: the crew orders it (tv16wide.h)
     const uint32_t nhelp = LONE ? A.helpers : 0u;
     CallCtl *const ccp = A.cc;
     const uint32_t tb = f2u(t);
     const uint32_t wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;
     const bool tail_in = tail && tail_key >= u2f(wlo);
-    bool fast = (flags & TV16_DEC_WIN) && N <= POS_LIM && Wtot + (tail_in ? 1u : 0u) > 0 && !(A.mode & 2u);
+    bool fast = (flags & TV16_DEC_WIN) && N <= POS_LIM && Wtot + (tail_in ? 1u : 0u) > 0 && A.mode != 2u &&
+                A.mode != 3u;
     if (!fast && tid == 0) {  // why the literal heap (debug words 60..63)
         if (!(flags & TV16_DEC_WIN)) atomicAdd(&A.dbg[60], 1u);
         if (N > POS_LIM) atomicAdd(&A.dbg[61], 1u);
@@ -921,7 +939,7 @@ tv16_fill(Tv16FillArgs A) {
                     }
                 }
             }
-            if ((__any(bad) || (A.mode & 1u)) && (tid & 63u) == 0) S.flag2 = 1;
+            if ((__any(bad) || A.mode == 1u) && (tid & 63u) == 0) S.flag2 = 1;
             __syncthreads();
             stamp(0);
             if (!S.flag2) {
@@ -1184,6 +1202,37 @@ tv16_fill(Tv16FillArgs A) {
         }
     }
     __syncthreads();
+    // the leader (tv16wide.h) over the window list, when the window holds the
+    // top min(P0 + 2, N) candidates (the ragged tail joins as an entry)
+    if ((flags & TV16_DEC_WIN) && A.mode != 2u) {
+        const uint32_t P0 = (rem + 15u) / 16u, seln = min(P0 + 1u, N - 1u);
+        if (Wtot >= seln + 1u || Wtot + (tail ? 1u : 0u) == N) {
+            WideLds &Wl = *reinterpret_cast<WideLds *>(fill_lds);
+            LeadIn I;
+            I.lk = cu;
+            I.lp = cl;
+            I.lc = ci;
+            I.n = Wtot;
+            I.tail = tail ? 1u : 0u;
+            I.tail_bits = f2u(tail_key);
+            I.N = N;
+            I.nb = d.nb;
+            I.rem = rem;
+            I.tl = d.tl;
+            I.g = reinterpret_cast<uint32_t *>(d.heap);
+            I.gcap = 2u * (d.nb + 64u);
+            const LeadOut O = leader(Wl, I);
+            if (O.ok) {
+                const uint32_t *const opos = O.ordpos;
+                emit_all<KE, LONE>(d, cnt, rem, O.P, O.tail_rank, [&](uint32_t i) { return ld_sc1(&opos[i]); }, nhelp,
+                                   ccp, order_g, ready_tag);
+                if (tid == 0) atomicAdd(&A.dbg[52], 1u);
+                return;
+            }
+            if (tid == 0) atomicAdd(&A.dbg[54], 1u);
+            __syncthreads();
+        }
+    }
     if (tid == 0) { S.flag = NONE; S.npop = 0; }
     __syncthreads();
     stamp(3);
@@ -1214,9 +1263,9 @@ hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {
                             (int)LFIN_LDS);
     if (attr0 != hipSuccess) return attr0;
     if (attr1 != hipSuccess) return attr1;
-    if (a.lfin) tv16_fill<true><<<a.workers + a.rankers, FILL_WG, LFIN_LDS, s>>>(a);
-    else if (a.lone) tv16_fill<true><<<a.nbk + a.helpers, FILL_WG, sizeof(FillLds), s>>>(a);
-    else tv16_fill<false><<<a.nbk, FILL_WG, sizeof(FillLds), s>>>(a);
+    if (a.lfin) tv16_fill<true><<<a.workers + a.rankers + a.crew, FILL_WG, LFIN_LDS, s>>>(a);
+    else if (a.lone) tv16_fill<true><<<a.nbk + a.helpers + a.crew, FILL_WG, sizeof(FillLds), s>>>(a);
+    else tv16_fill<false><<<a.nbk + a.crew, FILL_WG, sizeof(FillLds), s>>>(a);
     return hipGetLastError();
 }
 

@@ -93,8 +93,36 @@ constexpr uint32_t LMAXC = 4096;  // chunks of a bucket the one-bucket path take
 constexpr uint32_t LNBIN = 1024;
 constexpr uint32_t LBCAP = 32;
 
+// thresholdv16 regime-B crew (tv16wide.h): per bucket slot of a launch, the
+// level-1 histogram of the candidates' keys and the hand-offs between phases
+constexpr uint32_t CREW_BINS = 8192;
+struct CrewCtl {
+    uint32_t hist[CREW_BINS];  // zeroed by the bucket's phase Z
+    uint32_t beta, nL, status, P, tail_rank, op, pad[2];
+};
+
+// top-k in one launch (topk1.hip): per-call control block, two copies by call
+// tag parity (each call zeroes the next call's), and the band histogram
+constexpr uint32_t TK1_NPH = 13;    // phases
+constexpr uint32_t TK1_SH = 8;      // ticket / completion shards (tile % 8)
+constexpr uint32_t TK1_LINE = 32;   // words per 128-byte line: every shard counter on a line of its own
+constexpr uint32_t TK1_FINE = 8192; // band histogram bins
+constexpr uint32_t TK1_BINL = 2048; // entries of T's band bin listed (more: the select's way)
+struct alignas(128) TopkCtl {
+    uint32_t tk[TK1_NPH][TK1_SH][TK1_LINE];    // tickets per phase and shard
+    uint32_t done[TK1_NPH][TK1_SH][TK1_LINE];  // units done per phase and shard
+    uint32_t sdone[TK1_NPH][TK1_LINE];         // shards done per phase
+    uint32_t flag[TK1_NPH];                    // = the call tag once single-unit phase p is done
+    uint32_t miss, res_T, pick_bin, pick_rin, nbin_list;
+    uint32_t pad[TK1_LINE - TK1_NPH - 5];
+    uint2 binl[TK1_BINL];                      // {element, key} of T's band bin
+};
+
 struct DevWS {
     FillCtl *ctl;
+    TopkCtl *tkctl;      // [2]
+    uint32_t *tkfine;    // TK1_FINE words, zero between calls
+    CrewCtl *crew;       // MAX_BATCH slots
     ChunkDesc *desc;     // thresholdv16 chunk descriptors (grown per launch, zeroed)
     CallParams *cp;
     RSel *rsel;
@@ -161,7 +189,10 @@ struct Tv16FillArgs {
     const Decision *dec;
     uint32_t *fail;
     uint32_t *dbg;         // diagnostics: phase stamps of workgroup 0 (ws.misc)
-    uint32_t mode;         // tests (STG_DEBUG_TV16_FILL): 1 = always the shadow heap, 2 = always the literal heap
+    uint32_t mode;         // tests (STG_DEBUG_TV16_FILL): 1 = always the shadow heap, 2 = always the literal heap,
+                           // 3 = always the leader over the window, 4 = always the crew
+    uint32_t crew;         // extra workgroups that order window-miss buckets (tv16wide.h; 0: none)
+    CrewCtl *crew_ctl;     // MAX_BATCH slots
     bool lone;             // a one-bucket launch: the fill variant that takes the CU's registers
     uint32_t helpers;      // lone: extra workgroups that emit shares of the order (0: none)
     CallCtl *cc;           // this call's counters: [pad 0] fill tickets, [1] order ready, [2] pops, [3] tail rank,
@@ -235,6 +266,10 @@ struct TopkLaunch {
     hipEvent_t *ev;
 };
 hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s);
+// top-k in one launch steered by the key's last k-th magnitude (topk1.hip);
+// buckets of at most TOPK_LIST_TILES tiles
+hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, bool hinted, uint32_t tag,
+                        hipStream_t s);
 
 // Radix select: the key of descending rank `rank` among (bits(a[i]) & 0x7fffffff),
 // i < m, with the last element's bits additionally masked by `last_mask`, plus

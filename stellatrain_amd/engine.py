@@ -161,16 +161,27 @@ def scatter_merge_check(device=None) -> None:
     ``device`` hit a device failure (a look-back that gave up; the count of
     that call reads 0xffffffff).  Syncs the stream."""
     import torch
-    dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
-    check(lib().stg_scatter_merge_check(C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+    dev = _cuda_device(device)
+    with torch.cuda.device(dev):  # the C side keys the scratch on the current device
+        check(lib().stg_scatter_merge_check(C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
 
 
 def scatter_merge_release(device=None) -> None:
     """Frees the MERGE decompress scratch kept for the current stream of
     ``device`` (call before dropping a stream that merged)."""
     import torch
-    dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
-    check(lib().stg_scatter_merge_release(C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+    dev = _cuda_device(device)
+    with torch.cuda.device(dev):
+        check(lib().stg_scatter_merge_release(C.c_void_p(torch.cuda.current_stream(dev.index).cuda_stream)))
+
+
+def _cuda_device(device):
+    """torch.device of `device` (None or a bare "cuda": the current device)."""
+    import torch
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    d = torch.device(device)
+    return torch.device("cuda", torch.cuda.current_device() if d.index is None else d.index)
 
 
 def gather_slice(n: int, local_rank: int, num_gpus: int):

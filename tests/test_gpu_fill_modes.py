@@ -6,9 +6,13 @@ start positions (when its two checks pass), the shadow heap, or the literal
 make_heap / pop_heap in global memory.  A one-bucket call's finish
 (tv16lfin.h) first lets its rankers order the fill in parallel by the same
 right-first rule and falls back to that orderer when they cannot prove it.
-STG_DEBUG_TV16_FILL forces the heavier ways, so each is checked against the
-oracle on the same tie-heavy AIMD sequences; the path counters show which way
-ran.
+A bucket whose window below t misses the pops (a drop of the gradient scale)
+is ordered by the crew (tv16wide.h): extra workgroups of the fill launch list
+its top candidates again and the leader orders them; the leader also takes the
+orderer's calls its LDS paths cannot.  STG_DEBUG_TV16_FILL forces the heavier
+ways, so each is checked against the oracle on the same tie-heavy AIMD
+sequences (one-bucket calls and a batched launch, each ending in a 100x scale
+drop); the path counters show which way ran.
 """
 from __future__ import annotations
 
@@ -33,12 +37,15 @@ def _child(mode: int, **extra):
 
 
 def test_production_order(gpu):
-    """Every call here is one bucket: the one-bucket finish's rankers order
-    the regime-B fills (tv16lfin.h); D1's regime-B calls tie among the pops."""
+    """One-bucket calls: the one-bucket finish's rankers order the regime-B
+    fills (tv16lfin.h); D1's regime-B calls tie among the pops.  The scale
+    drops are window misses: the crew orders them, never the literal heap."""
     out = _child(0)
     plain, tied, viol, notake = out["lfin"]
     assert tied > 0, out
     assert out["paths"][3] == 0, out  # never the literal heap
+    leader, crew, leader_lit, crew_lit = out["wide"]
+    assert crew > 0 and leader_lit == 0 and crew_lit == 0, out
 
 
 def test_production_order_orderer_alone(gpu):
@@ -68,3 +75,22 @@ def test_literal_heap_order(gpu):
     out = _child(2)
     none, by_start, shadow, literal = out["paths"]
     assert by_start == 0 and shadow == 0 and literal > 0, out
+    assert out["wide"] == [0, 0, 0, 0], out
+
+
+def test_leader_order(gpu):
+    """The leader over the window list on every regime-B call the window
+    holds (the orderer's fast paths skipped); the crew for the misses."""
+    out = _child(3)
+    none, by_start, shadow, literal = out["paths"]
+    leader, crew, leader_lit, crew_lit = out["wide"]
+    assert by_start == 0 and shadow == 0 and literal == 0, out
+    assert leader > 0 and crew > 0 and leader_lit == 0 and crew_lit == 0, out
+
+
+def test_crew_order(gpu):
+    """The crew on every regime-B bucket (window or not)."""
+    out = _child(4)
+    none, by_start, shadow, literal = out["paths"]
+    leader, crew, leader_lit, crew_lit = out["wide"]
+    assert literal == 0 and leader == 0 and crew > 0 and crew_lit == 0, out

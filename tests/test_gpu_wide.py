@@ -1,0 +1,82 @@
+"""The regime-B fill past the window (tv16wide.h), at full size.
+
+A 100x drop of the gradient scale leaves every line sum of a 64 MiB bucket far
+below the window the scan lists under t, and AIMD decays t by only 1 % per
+call (thresholdv16.cpp:243-259): the crew re-reads the bucket, lists its top
+candidates and the leader orders the pops -- bounded, where the literal heap
+took ~45 ms per call.  A bucket of 2^25 + 13 floats has more than 2^20 lines,
+past the orderer's 20-bit heap keys: every regime-B call goes to the leader or
+the crew.  Whole streams against the oracle (the reference's algorithm,
+pinned to oracle/_ref), count and threshold bits included.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from parity import assert_same_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _words(comp, stream):
+    from stellatrain_amd._capi import check, lib
+    w = (C.c_uint32 * 64)()
+    check(lib().stg_codec_debug_words(comp._h, C.c_void_p(stream.cuda_stream), w, 64))
+    return list(w)
+
+
+def _run(gpu, oracle, n, calls, drop_from, seed):
+    import torch
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel
+    comp = ThresholdvCompressor16()
+    ho = oracle.tv16_new()
+    k = merge_numel(n, 0.99)
+    idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+    val = torch.zeros(k, dtype=torch.float32, device=gpu)
+    regimes, times = [], []
+    try:
+        for c in range(calls):
+            x = oracle.synth(n, seed + c)
+            if c >= drop_from:
+                x = x * np.float32(0.01)
+            d = torch.from_numpy(x).to(gpu)
+            t_before = oracle.tv16_state(ho, "w@weight")
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            cnt = comp.compress("w@weight", d, k, idx, val)
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) * 1e3)
+            co, io, vo = oracle.tv16_compress(ho, "w@weight", x, k)
+            assert cnt == co, (c, cnt, co)
+            assert_same_stream(idx.cpu().numpy().view(np.uint32), val.cpu().numpy(), io, vo, co)
+            t_after = oracle.tv16_state(ho, "w@weight")
+            assert np.float32(comp.state("w@weight")[0]).view(np.uint32) == np.float32(t_after[0]).view(np.uint32)
+            regimes.append("-" if t_before is None else "B" if t_after[0] < t_before[0] else "A")
+        comp.check_device()
+        w = _words(comp, torch.cuda.current_stream(gpu))
+    finally:
+        oracle.tv16_free(ho)
+    return regimes, times, w
+
+
+def test_scale_drop_64mib(gpu, oracle):
+    """A converged 64 MiB key, then three calls at 1/100 scale: window misses,
+    ordered by the crew; never the literal heap."""
+    regimes, times, w = _run(gpu, oracle, 16 << 20, 7, 4, 9100)
+    print("regimes", regimes, "us", [round(t, 1) for t in times], "wide", w[52:56], "paths", w[56:60])
+    assert regimes[4:] == ["B"] * 3, regimes
+    assert w[53] >= 3 and w[55] == 0 and w[59] == 0, w[48:64]
+
+
+def test_bucket_past_2p20_lines(gpu, oracle):
+    """2^25 + 13 floats (2,097,152 lines and a 13-float tail), an AIMD
+    sequence through both regimes (and a scale drop at the end)."""
+    regimes, times, w = _run(gpu, oracle, (1 << 25) + 13, 8, 6, 9300)
+    print("regimes", regimes, "us", [round(t, 1) for t in times], "wide", w[52:56], "paths", w[56:60])
+    assert "A" in regimes[:6] and "B" in regimes[:6], regimes
+    assert w[59] == 0 and w[54] == 0 and w[55] == 0, w[48:64]

@@ -60,6 +60,14 @@ for s in "$@"; do
         prof_merge) step prof_merge 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_merge" -o run -- python3 tools/bench_configs.py --only merge
             python3 tools/ktrace.py gpurun_out/prof_merge 16 > gpurun_out/prof_merge.txt 2>&1 ;;
         scale_drop) step scale_drop 280 python tools/scale_drop.py 4 ;;
+        fill_paths) step fill_paths 200 python tools/fill_paths.py --steps 400 ;;
+        stamps_r4) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_tk1st.so step tk1_stamps 150 python tools/tk1_stamps.py
+            STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_crewst.so step crew_stamps 150 python tools/crew_stamps.py ;;
+        tiny) step tiny 120 python tools/tiny_probe.py
+            STG_TV16_CREW_LONE=0 step tiny_nocrew 120 python tools/tiny_probe.py
+            STG_DEBUG_TV16_FILL=2 step tiny_literal 120 python tools/tiny_probe.py ;;
+        tests_topk1) step tests_topk1 600 python -u -m pytest tests/test_gpu_topk1.py tests/test_gpu_codecs.py tests/test_gpu_configs.py -k "topk or c2 or hint" -v -m gpu --timeout 300 --timeout-method thread ;;
+        tests_wide) step tests_wide 600 python -u -m pytest tests/test_gpu_wide.py tests/test_gpu_fill_modes.py -v -s -m gpu --timeout 300 --timeout-method thread ;;
         c2ab)  # shipped-mode top-k: the ordered six-launch path (STG_TOPK_BK=0) against the unordered three
             STG_TOPK_BK=0 step c2_ordered 150 python tools/bench_configs.py --only topk --cpu-seconds 0
             step c2_bk 150 python tools/bench_configs.py --only topk --cpu-seconds 0
