@@ -732,10 +732,13 @@ uint32_t crew_batch() {
     static const uint32_t v = getenv("STG_TV16_CREW") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW"))) : 64u;
     return v ? std::min(std::max(v, MAX_BATCH + 1u), 1024u) : 0u;  // > MAX_BATCH: see tv16wide.h crew_loop
 }
-uint32_t crew_lone() {
+// One-bucket launches: every CU the launch's other workgroups leave (a fill
+// workgroup takes a whole CU's LDS), so that phase A streams at full width.
+uint32_t crew_lone(uint32_t num_cu, uint32_t others) {
     static const uint32_t v =
-        getenv("STG_TV16_CREW_LONE") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW_LONE"))) : 128u;
-    return v ? std::min(std::max(v, MAX_BATCH + 1u), 1024u) : 0u;
+        getenv("STG_TV16_CREW_LONE") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW_LONE"))) : 1024u;
+    const uint32_t room = num_cu > others ? num_cu - others : 0u;
+    return v ? std::min(std::max(std::min(v, room), MAX_BATCH + 1u), 1024u) : 0u;
 }
 
 }  // namespace
@@ -855,7 +858,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.state = a.b[0].state;
         F.cp = ws.cp;
         F.resid = a.b[0].resid;
-        F.crew = crew_lone();
+        F.crew = crew_lone(a.num_cu, workers + rankers);
         F.crew_ctl = ws.crew;
         if ((e = launch_tv16_fill(F, s)) != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[2], s);
@@ -891,7 +894,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
         F.helpers = F.lone ? std::min(helpers, 63u) : 0u;
         F.cc = &ws.ctl->cc[a.epoch & 1u];
-        F.crew = F.lone ? crew_lone() : crew_batch();
+        F.crew = F.lone ? crew_lone(a.num_cu, F.nbk + F.helpers) : crew_batch();
         F.crew_ctl = ws.crew;
         const hipError_t e = launch_tv16_fill(F, s);
         if (e != hipSuccess) return e;

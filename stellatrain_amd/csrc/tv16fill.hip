@@ -1220,6 +1220,9 @@ tv16_fill(Tv16FillArgs A) {
             I.rem = rem;
             I.tl = d.tl;
             I.g = reinterpret_cast<uint32_t *>(d.heap);
+            I.dbg = A.dbg;
+            I.lvl1 = NONE;
+            I.r1 = 0;
             I.gcap = 2u * (d.nb + 64u);
             const LeadOut O = leader(Wl, I);
             if (O.ok) {

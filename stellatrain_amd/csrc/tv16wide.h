@@ -34,12 +34,14 @@
 // window just below t) has its top candidates nowhere, so extra workgroups of
 // the fill launch, each taking units in ticket order, find them again:
 //   Z  zero the bucket's level-1 histogram                              (1 unit)
-//   A  stream 4,096 lines: line sums in the scan's AVX tree order, the ordered
-//      key of each line (0 for a qualifying line) into the scratch, the
-//      candidates' histogram of the key's top 13 bits, qualifying count  (nb / 4096)
-//   B  pick the bin holding the (min(P0 + 1, N - 1) + 1)-th largest key  (1 unit)
-//   C  list every candidate in that bin or above, in scan order, with its
-//      candidate index (look-back over the units' tagged counts)          (nb / 16384)
+//   A  stream la lines (la: the bucket over the crew): line sums in the
+//      scan's AVX tree order, the ordered key of each line (0 for a
+//      qualifying line) into the scratch, the candidates' histogram of the
+//      key's top 13 bits                                                 (nb / la)
+//   C  pick the bin holding the (min(P0 + 1, N - 1) + 1)-th largest key
+//      (every unit, from the histogram), list every candidate in that bin
+//      or above, in scan order, with its candidate index (look-back over
+//      the units' tagged counts)                                         (nb / 16384)
 //   D  the leader over the list                                          (1 unit)
 //   E  emit the pops                                                     (32 units)
 // A unit waits only for units with smaller tickets (the previous phase of its
@@ -55,22 +57,22 @@ constexpr uint32_t WHL = 6;       // a late line's subtree: its ancestor 6 level
 constexpr uint32_t WROOTS = 64;   // replayed subtrees at most
 constexpr uint32_t WRUN = 512;    // equal sums re-ordered after a replay at most
 constexpr uint32_t WRFD = 27;     // rf32: heap positions < 2^28 - 1
-constexpr uint32_t CW_LA = 4096;  // crew phase A: lines per unit (256 KiB)
-constexpr uint32_t CW_LC = 16384; // crew phase C: keys per unit (32 per thread)
+constexpr uint32_t CW_LA = 2048;  // crew phase A: lines per unit at least (128 KiB)
+constexpr uint32_t CW_LC = 8192;  // crew phase C: keys per unit (16 per thread)
 constexpr uint32_t CW_NE = 32;    // crew phase E: emission units
 constexpr uint32_t CW_DA = 6;     // crew phase A: float4 loads in flight per lane
-constexpr uint32_t CW_PH = 6;     // phases Z A B C D E
+constexpr uint32_t CW_PH = 5;     // phases Z A C D E
 constexpr uint32_t LNONE = 0x7fffffffu;
 #ifndef STG_CREW_STAMPS
-#define STG_CREW_STAMPS 0  // diagnostics: crew phase completion times (100 MHz clock), debug words 16..22
+#define STG_CREW_STAMPS 0  // diagnostics: crew phase completion times (100 MHz clock), debug words 16..23
 #endif
-static_assert(CW_LC == 32 * FILL_WG && CW_LC % CW_LA == 0, "phase C: 32 keys per thread, whole A units");
+static_assert(CW_LC == 16 * FILL_WG && CW_LC <= 0xffffu, "phase C: 16 keys per thread; 16-bit unit counts");
 
 // A window-miss bucket as the crew sees it.
 struct CrewBk {
     Tv16FillBucket d;
     uint32_t slot, cnt, rem, N, tbits, tail, tail_bits;
-    uint32_t nA, nC;
+    uint32_t la, nA, nC;  // A: lines per unit, units; C: units
 };
 
 // LDS of the leader and the crew (a view of the fill launch's dynamic LDS).
@@ -115,12 +117,14 @@ struct LeadIn {
     uint32_t N, nb, rem, tl;
     uint32_t *g;                   // scratch words (8-byte aligned)
     uint32_t gcap;
+    uint32_t *dbg;                 // stamp builds: the leader's step times, words 24..28
+    uint32_t lvl1, r1;             // lvl1 != NONE: the key at rank sel has top 13 bits lvl1, rank r1 among them
 };
 struct LeadOut {
     bool ok;
     uint32_t P, tail_rank;
     const uint32_t *ordpos;  // element position of each pop
-    uint32_t why;            // failure: 1 NaN, 2 scratch, 3 crowded bin, 4 short list, 5 roots, 6 height, 7 late, 8 run
+    uint32_t why;            // failure: 1 NaN, 2 scratch, 3 crowded bin / rank not found, 4 short list, 5 roots, 6 height, 7 late, 8 run
 };
 
 // Bounded poll by thread 0 until *w >= target; every thread gets the verdict.
@@ -128,8 +132,10 @@ __device__ __forceinline__ bool wide_wait(uint32_t *w, uint32_t target, uint32_t
     if (threadIdx.x == 0) {
         uint32_t ok = 1;
         uint64_t st = 0;
+        uint32_t nap = 1;  // backing off: many waiters on one line slow everyone's memory path
         for (uint32_t sp = 0; ld_sc1(w) < target; ++sp) {
-            __builtin_amdgcn_s_sleep(4);
+            for (uint32_t k = 0; k < nap; ++k) __builtin_amdgcn_s_sleep(4);
+            nap = min(2u * nap, 16u);
             if (spin_expired(sp, st)) { ok = 0; break; }
         }
         *flag = ok;
@@ -140,91 +146,175 @@ __device__ __forceinline__ bool wide_wait(uint32_t *w, uint32_t target, uint32_t
     return r;
 }
 
-// Batched loops: each thread loads WB entries (all in flight), then uses them
+// Batched loops: each thread loads B entries (all in flight), then uses them
 // -- a loop whose every iteration waits for its own load runs at one L2 round
-// trip per iteration.
+// trip per iteration.  The loads are unconditional (an index past the end
+// loads entry n - 1 again): a load under a branch gets a wait for it at the
+// branch's join, which serialises the batch again.  ld must not branch either.
 constexpr uint32_t WB = 8;
-template <typename V, typename Ld, typename Use>
+template <typename V, uint32_t B = WB, typename Ld, typename Use>
 __device__ __forceinline__ void each_b(uint32_t n, Ld ld, Use use) {
-    for (uint32_t i0 = 0; i0 < n; i0 += WB * FILL_WG) {
-        V v[WB];
+    for (uint32_t i0 = 0; i0 < n; i0 += B * FILL_WG) {
+        V v[B];
 #pragma unroll
-        for (uint32_t b = 0; b < WB; ++b) {
-            const uint32_t i = i0 + b * FILL_WG + threadIdx.x;
-            if (i < n) v[b] = ld(i);
-        }
+        for (uint32_t b = 0; b < B; ++b) v[b] = ld(min(i0 + b * FILL_WG + threadIdx.x, n - 1u));
 #pragma unroll
-        for (uint32_t b = 0; b < WB; ++b) {
+        for (uint32_t b = 0; b < B; ++b) {
             const uint32_t i = i0 + b * FILL_WG + threadIdx.x;
             if (i < n) use(i, v[b]);
         }
     }
 }
+// ... with a second load that depends on the first (two round trips per batch)
+template <typename V1, typename V2, typename Ld1, typename Ld2, typename Use>
+__device__ __forceinline__ void each_b2(uint32_t n, Ld1 ld1, Ld2 ld2, Use use) {
+    for (uint32_t i0 = 0; i0 < n; i0 += WB * FILL_WG) {
+        V1 a[WB];
+        V2 v[WB];
+#pragma unroll
+        for (uint32_t b = 0; b < WB; ++b) a[b] = ld1(min(i0 + b * FILL_WG + threadIdx.x, n - 1u));
+#pragma unroll
+        for (uint32_t b = 0; b < WB; ++b) v[b] = ld2(min(i0 + b * FILL_WG + threadIdx.x, n - 1u), a[b]);
+#pragma unroll
+        for (uint32_t b = 0; b < WB; ++b) {
+            const uint32_t i = i0 + b * FILL_WG + threadIdx.x;
+            if (i < n) use(i, a[b], v[b]);
+        }
+    }
+}
+struct KC4 {
+    u4v k, c;  // four list entries: sum bits, candidate indices
+};
+struct Adj {
+    uint32_t o, o2;  // two neighbours of R: entries (with the tie bit)
+    uint64_t s, s2;  // ... their composite keys
+};
+// the heap position of a right-first key (the inverse of rf32)
+__device__ __forceinline__ uint32_t rf_pos(uint32_t r) {
+    const uint32_t d = r & 31u, inv = (r >> 5) >> (WRFD - d), mk = (1u << d) - 1u;
+    return ((1u << d) | (~inv & mk)) - 1u;
+}
+
+// plain loads (see the leader)
+__device__ __forceinline__ uint32_t ldc(const uint32_t *p) { return *p; }
+__device__ __forceinline__ uint64_t ldc(const uint64_t *p) { return *p; }
+
+#define LEAD_STAMP(i)                                                                                       \
+    do {                                                                                                    \
+        if (STG_CREW_STAMPS && threadIdx.x == 0) I.dbg[24 + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+// finer steps (stamp builds): words 8..15, and the list / R sizes in 6, 7
+#define LEAD_SUB(i)                                                                                         \
+    do {                                                                                                    \
+        if (STG_CREW_STAMPS && threadIdx.x == 0) I.dbg[8 + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 // The leader: the pops of a regime-B fill over a candidate list that holds
 // every candidate of the top min(P0 + 2, N) (P0 = ceil(rem / 16)); candidates
-// not listed have smaller sums than every listed one of R.  One workgroup.
+// not listed have smaller sums than every listed one of R.  One workgroup;
+// every pass over global data keeps WB loads per thread in flight (the list as
+// 16-byte loads), and lookups by candidate index go through an LDS sample.
 __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
     LeadOut O;
     O.ok = false;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t m = I.n + I.tail;
-    auto kb = [&](uint32_t i) -> uint32_t { return i < I.n ? ld_sc1(&I.lk[i]) : I.tail_bits; };
-    auto cx = [&](uint32_t i) -> uint32_t { return i < I.n ? ld_sc1(&I.lc[i]) : I.N - 1u; };
-    auto ps = [&](uint32_t i) -> uint32_t { return i < I.n ? ld_sc1(&I.lp[i]) : I.nb * 16u; };
     O.P = 0;
     O.tail_rank = NONE;
     O.why = 0;
+    const uint32_t tid = threadIdx.x;
+    // Loads go through this XCD's L2 (cached: the list and the scratch are
+    // read many times); the acquire drops lines other XCDs have since written.
+    // Stores stay sc1 (write-through: the L2 line and memory both updated).
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t n = uni(I.n), tail = uni(I.tail), tbits = uni(I.tail_bits), NN = uni(I.N);
+    const uint32_t m = n + tail;
+    const uint32_t *const lk = uni_ptr(I.lk), *const lp = uni_ptr(I.lp), *const lc = uni_ptr(I.lc);
     if (!m) { O.ok = true; return O; }
-    if ((size_t)6 * m + 8 > I.gcap || I.N >= (1u << 28)) { O.why = 2; return O; }
-    uint64_t *const gk = reinterpret_cast<uint64_t *>(I.g);
-    uint32_t *const gi = I.g + 2 * (size_t)m, *const go = gi + m, *const gp = go + m, *const op = gp + m;
-    const uint32_t P0 = (I.rem + 15u) / 16u;
+    // entry i (i == n: the tail); branch-free (see each_b)
+    const uint32_t nl = n ? n - 1u : 0u, tpos = uni(I.nb) * 16u;
+    auto kb = [&](uint32_t i) -> uint32_t { const uint32_t x = ldc(&lk[min(i, nl)]); return i < n ? x : tbits; };
+    auto cx = [&](uint32_t i) -> uint32_t { const uint32_t x = ldc(&lc[min(i, nl)]); return i < n ? x : NN - 1u; };
+    auto ps = [&](uint32_t i) -> uint32_t { const uint32_t x = ldc(&lp[min(i, nl)]); return i < n ? x : tpos; };
+    if ((size_t)6 * m + 8 > uni(I.gcap) || NN >= (1u << 28)) { O.why = 2; return O; }
+    uint32_t *const g = uni_ptr(I.g);
+    // R in order: entries (with the tie bit), composite keys; positions; the pops' positions
+    uint32_t *const go = g, *const gp = go + m, *const op = gp + m;
+    uint64_t *const gs = reinterpret_cast<uint64_t *>(g + 4 * (size_t)m);
+    const uint32_t *const gs32 = reinterpret_cast<const uint32_t *>(gs);
+    const uint32_t P0 = (uni(I.rem) + 15u) / 16u;
     const uint32_t sel = min(P0 + 1u, m - 1u);
     uint32_t *const hist = W.u.s.hist;
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(lk), 0, n * 4u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(lc), 0, n * 4u, 0x00020000);
+    const uint32_t nq = (n + 3u) / 4u;
+    auto ld4 = [&](__amdgpu_buffer_rsrc_t r, uint32_t q) -> u4v {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, q * 16u, 0, 0);
+    };
+    auto keys4 = [&](auto use) {  // use(entry, sum bits) for every entry
+        each_b<u4v>(nq, [&](uint32_t q) { return ld4(rk, q); }, [&](uint32_t q, u4v x) {
+            const uint32_t i = 4u * q;
+            use(i, x.x);
+            if (i + 1u < n) use(i + 1u, x.y);
+            if (i + 2u < n) use(i + 2u, x.z);
+            if (i + 3u < n) use(i + 3u, x.w);
+        });
+        if (tail && tid == 0) use(n, tbits);
+    };
 
-    // ---- 1. the key at descending rank sel: three radix levels (11, 11, 10 bits) ----
+    // ---- 1. the key at descending rank sel: radix levels of 11, 11 and 10
+    //      bits, the first skipped when the caller knows the top 13 bits ----
+    uint32_t pre = 0, pm = 0, r = sel, p0 = 0;
+    if (uni(I.lvl1) != NONE) {
+        pre = uni(I.lvl1) << WSH;
+        pm = ~((1u << WSH) - 1u);
+        r = uni(I.r1);
+        p0 = 1;
+    }
     if (tid == 0) { W.v[0] = 0; W.v[1] = 0; }
-    uint32_t pre = 0, pm = 0, r = sel;
-    for (uint32_t pass = 0; pass < 3; ++pass) {
+    for (uint32_t pass = p0; pass < 3; ++pass) {
         const uint32_t sh = pass == 0 ? 21u : pass == 1 ? 10u : 0u, nbin = pass == 2 ? 1024u : 2048u;
+        const bool first = pass == p0;
         for (uint32_t b = tid; b < nbin; b += FILL_WG) hist[b] = 0;
+        if (tid == 0) W.v[2] = NONE;
         __syncthreads();
         uint32_t kmx = 0, nanf = 0;
-        each_b<uint32_t>(m, kb, [&](uint32_t, uint32_t b) {
+        keys4([&](uint32_t, uint32_t b) {
             const uint32_t k = okey(b);
-            nanf |= nan_bits(b) ? 1u : 0u;
-            kmx = max(kmx, k);
+            if (first) {
+                nanf |= nan_bits(b) ? 1u : 0u;
+                kmx = max(kmx, k);
+            }
             if ((k & pm) == pre) atomicAdd(&hist[(k >> sh) & (nbin - 1u)], 1u);
         });
-        if (pass == 0) {
+        if (first) {
             kmx = wave_max(kmx);
             if ((tid & 63u) == 0) atomicMax(&W.v[1], kmx);
             if (nanf) W.v[0] = 1;
         }
         __syncthreads();
         const uint32_t per = nbin / FILL_WG;  // 4 or 2 bins per thread, highest first
-        uint32_t c[4], s = 0;
+        uint32_t c[8], s = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
+        for (uint32_t u = 0; u < 8; ++u) {
             c[u] = u < per ? hist[nbin - 1u - (per * tid + u)] : 0u;
             s += c[u];
         }
         uint32_t tot;
         uint32_t a = blk_excl_scan<FNW_F>(s, W.sh, &tot);
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
+        for (uint32_t u = 0; u < 8; ++u) {
             if (u < per && a <= r && r < a + c[u]) { W.v[2] = nbin - 1u - (per * tid + u); W.v[3] = r - a; }
             a += c[u];
         }
         __syncthreads();
-        pre |= W.v[2] << sh;
+        if (W.v[0]) { O.why = 1; return O; }
+        if (W.v[2] == NONE) { O.why = 3; return O; }
+        pre |= uni(W.v[2]) << sh;
         pm |= (nbin - 1u) << sh;
-        r = W.v[3];
+        r = uni(W.v[3]);
         __syncthreads();
     }
-    if (W.v[0]) { O.why = 1; return O; }
-    const uint32_t okS = pre, kmax = W.v[1];
+    const uint32_t okS = uni(pre), kmax = uni(W.v[1]);
+    LEAD_STAMP(0);
 
     // ---- 2. R = {key >= okS} by (key desc, rf32(start) asc): counting sort
     //      into bins of the key's distance below the maximum, then ranks
@@ -234,14 +324,16 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
     if (tid == 0) { W.v[4] = 0; W.v[5] = 0; }
     __syncthreads();
     uint32_t nr = 0;
-    each_b<uint32_t>(m, kb, [&](uint32_t, uint32_t b) {
+    keys4([&](uint32_t, uint32_t b) {
         const uint32_t k = okey(b);
         if (k >= okS) { atomicAdd(&hist[(kmax - k) >> shb], 1u); ++nr; }
     });
     nr = wave_sum(nr);
     if ((tid & 63u) == 0) atomicAdd(&W.v[4], nr);
     __syncthreads();
-    nr = W.v[4];
+    nr = uni(W.v[4]);
+    LEAD_SUB(0);
+    if (STG_CREW_STAMPS && tid == 0) { I.dbg[6] = m; I.dbg[7] = nr; }
     {   // exclusive scan of the bins (16 per thread), and the largest bin
         uint32_t c[16], s = 0, mx = 0;
 #pragma unroll
@@ -264,34 +356,45 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
         __syncthreads();
     }
     if (W.v[5] > WTILE) { O.why = 3; return O; }
-    each_b<uint2>(m, [&](uint32_t i) { return make_uint2(kb(i), cx(i)); }, [&](uint32_t i, uint2 x) {
-        const uint32_t k = okey(x.x);
-        if (k < okS) return;
-        const uint32_t slot = atomicAdd(&hist[(kmax - k) >> shb], 1u);
-        st_sc1(&gk[slot], ((uint64_t)(kmax - k) << 32) | rf32(x.y));
-        st_sc1(&gi[slot], i);
-    });
-    vm_drain();
-    __syncthreads();  // hist[b]: the end of bin b
+    LEAD_SUB(1);
+    // hist[b]: the start of bin b.  Tiles of whole bins: one pass over the
+    // list (cached loads) places the tile's entries in LDS, where they are
+    // ranked; only the ranked entries are stored (no load waits behind them).
     uint32_t tie_any = 0;
     for (uint32_t s0 = 0, b0 = 0; s0 < nr;) {
-        if (tid == 0) {  // the last bin b1 - 1 with end <= s0 + WTILE
+        if (tid == 0) {  // the largest b1 <= nbin with start(b1) <= s0 + WTILE (start(nbin) = nr)
             uint32_t lo = b0 + 1u, hi = nbin;
             while (lo < hi) {
                 const uint32_t md = (lo + hi + 1u) >> 1;
-                if (hist[md - 1u] <= s0 + WTILE) lo = md; else hi = md - 1u;
+                if ((md < nbin ? hist[md] : nr) <= s0 + WTILE) lo = md; else hi = md - 1u;
             }
             W.v[6] = lo;
         }
         __syncthreads();
-        const uint32_t b1 = W.v[6], s1 = hist[b1 - 1u], nt = s1 - s0;
-        each_b<uint64_t>(nt, [&](uint32_t j) { return ld_sc1(&gk[s0 + j]); }, [&](uint32_t j, uint64_t x) { W.u.s.tk[j] = x; });
-        each_b<uint32_t>(nt, [&](uint32_t j) { return ld_sc1(&gi[s0 + j]); }, [&](uint32_t j, uint32_t x) { W.u.s.ti[j] = x; });
-        __syncthreads();
+        const uint32_t b1 = uni(W.v[6]), s1 = uni(b1 < nbin ? hist[b1] : nr);
+        auto put = [&](uint32_t i, uint32_t bits, uint32_t c) {
+            const uint32_t k = okey(bits);
+            const uint32_t b = (kmax - k) >> shb;
+            if (k < okS || b < b0 || b >= b1) return;
+            const uint32_t slot = atomicAdd(&hist[b], 1u) - s0;
+            W.u.s.tk[slot] = ((uint64_t)(kmax - k) << 32) | rf32(c);
+            W.u.s.ti[slot] = i;
+        };
+        each_b<KC4, 4>(nq, [&](uint32_t q) { KC4 x; x.k = ld4(rk, q); x.c = ld4(rc, q); return x; }, [&](uint32_t q, KC4 x) {
+            const uint32_t i = 4u * q;
+            put(i, x.k.x, x.c.x);
+            if (i + 1u < n) put(i + 1u, x.k.y, x.c.y);
+            if (i + 2u < n) put(i + 2u, x.k.z, x.c.z);
+            if (i + 3u < n) put(i + 3u, x.k.w, x.c.w);
+        });
+        if (tail && tid == 0) put(n, tbits, NN - 1u);
+        __syncthreads();  // hist[b], b0 <= b < b1: the end of bin b
+        if (s0 == 0) LEAD_SUB(6);
+        const uint32_t nt = s1 - s0;
         for (uint32_t j = tid; j < nt; j += FILL_WG) {
             const uint64_t key = W.u.s.tk[j];
             const uint32_t b = (uint32_t)(key >> 32) >> shb;
-            const uint32_t lo = (b ? hist[b - 1u] : 0u) - s0, hi = hist[b] - s0;
+            const uint32_t lo = (b > b0 ? hist[b - 1u] : s0) - s0, hi = hist[b] - s0;
             uint32_t rk = s0 + lo;
             bool tie = false;
             for (uint32_t x = lo; x < hi; ++x) {
@@ -301,70 +404,114 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
             }
             tie_any |= tie ? 1u : 0u;
             st_sc1(&go[rk], W.u.s.ti[j] | (tie ? 0x80000000u : 0u));
+            st_sc1(&gs[rk], key);
         }
         __syncthreads();
+        if (s0 == 0) LEAD_SUB(7);
         s0 = s1;
         b0 = b1;
     }
     vm_drain();
     const bool ties = __syncthreads_or((int)tie_any);
+    LEAD_STAMP(2);
 
     // ---- 3. runs of equal sums: start positions one above the other, or a
     //      late line of R_s with an R_s line beside it -> replay those subtrees ----
-    const uint32_t late_lo = I.N > sel + 2u ? I.N - (sel + 2u) : 0u;
+    const uint32_t late_lo = NN > sel + 2u ? NN - (sel + 2u) : 0u;
     if (ties) {
         uint32_t dmx = 0;  // the lowest tied key (largest distance below kmax)
-        each_b<uint32_t>(nr, [&](uint32_t rr) { return ld_sc1(&go[rr]); }, [&](uint32_t, uint32_t o) {
-            if (o >> 31) dmx = max(dmx, kmax - okey(kb(o & LNONE)));
-        });
+        each_b<uint2>(nr, [&](uint32_t rr) { return make_uint2(ldc(&go[rr]), ldc(&gs32[2u * rr + 1u])); },
+                      [&](uint32_t, uint2 x) { if (x.x >> 31) dmx = max(dmx, x.y); });
         dmx = wave_max(dmx);
         if (tid == 0) { W.v[7] = 0; W.v[8] = 0; }
         __syncthreads();
         if ((tid & 63u) == 0) atomicMax(&W.v[7], dmx);
         __syncthreads();
-        const uint32_t ksm = kmax - W.v[7];  // R_smin = {key >= ksm}
+        dmx = uni(W.v[7]);
+        LEAD_SUB(2);
+        const uint32_t ksm = kmax - dmx;  // R_smin = {key >= ksm} = R's entries at distance <= dmx
         auto add_root = [&](uint32_t a) {
             const uint32_t x = atomicAdd(&W.v[8], 1u);
             if (x < WROOTS) W.roots[x] = a;
         };
         // (a) adjacent members of a run (rf32 order): the second below the first
-        for (uint32_t rr = tid; rr + 1u < nr; rr += FILL_WG) {
-            const uint32_t o = ld_sc1(&go[rr]), o2 = ld_sc1(&go[rr + 1u]);
-            if (!(o >> 31) || !(o2 >> 31)) continue;
-            const uint32_t e = o & LNONE, f = o2 & LNONE;
-            if (okey(kb(e)) != okey(kb(f))) continue;
-            const uint32_t ce = cx(e), cf = cx(f);
-            if (is_desc(cf + 1u, ce + 1u)) add_root(ce);
-        }
-        // (b) late lines of R_smin (start >= late_lo) with an R_smin line at the parent or sibling
-        auto lower = [&](uint32_t c) {  // first entry with candidate index >= c
-            uint32_t lo = 0, hi = m;
+        each_b<Adj>(nr ? nr - 1u : 0u,
+                    [&](uint32_t rr) {
+                        Adj a;
+                        a.o = ldc(&go[rr]);
+                        a.o2 = ldc(&go[rr + 1u]);
+                        a.s = ldc(&gs[rr]);
+                        a.s2 = ldc(&gs[rr + 1u]);
+                        return a;
+                    },
+                    [&](uint32_t, Adj a) {
+                        if (!(a.o >> 31) || !(a.o2 >> 31) || (uint32_t)(a.s >> 32) != (uint32_t)(a.s2 >> 32)) return;
+                        const uint32_t ce = rf_pos((uint32_t)a.s), cf = rf_pos((uint32_t)a.s2);
+                        if (is_desc(cf + 1u, ce + 1u)) add_root(ce);
+                    });
+        // lookups by candidate index: the list is in candidate order; smp[j] = cx(j S)
+        const uint32_t S = (m + WTILE - 1u) / WTILE, ns = (m + S - 1u) / S;
+        LEAD_SUB(3);
+        uint32_t *const smp = W.u.s.ti;  // (past the replay's LDS)
+        each_b<uint32_t>(ns, [&](uint32_t j) { return cx(j * S); }, [&](uint32_t j, uint32_t c) { smp[j] = c; });
+        __syncthreads();
+        auto lower = [&](uint32_t c) -> uint2 {  // the first entry with candidate index >= c, and that index
+            uint32_t lo = 0, hi = ns;
             while (lo < hi) {
                 const uint32_t md = (lo + hi) >> 1;
-                if (cx(md) < c) lo = md + 1u; else hi = md;
+                if (smp[md] < c) lo = md + 1u; else hi = md;
             }
-            return lo;
+            if (lo == 0) return make_uint2(0u, smp[0]);
+            const uint32_t base = (lo - 1u) * S, end = min(lo * S, m);  // cx(base) < c <= cx(end)
+            uint32_t rr = end, rcx = lo < ns ? smp[lo] : NONE;
+            for (uint32_t i0 = base + 1u; i0 < end && rr == end; i0 += 8u) {
+                uint32_t v[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u) {
+                    const uint32_t x = cx(min(i0 + u, end - 1u));
+                    v[u] = i0 + u < end ? x : NONE;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u)
+                    if (rr == end && v[u] != NONE && v[u] >= c) { rr = i0 + u; rcx = v[u]; }
+            }
+            return make_uint2(rr, rcx);
         };
         auto member = [&](uint32_t c) {
-            const uint32_t i = lower(c);
-            return i < m && cx(i) == c && okey(kb(i)) >= ksm;
+            const uint2 f = lower(c);
+            return f.x < m && f.y == c && okey(kb(f.x)) >= ksm;
         };
-        if (tid == 0) W.v[9] = lower(late_lo);
+        // (b) late lines of R_smin (start >= late_lo) with an R_smin line at
+        //     the parent or sibling: the late lines listed first (in the
+        //     replay's LDS, free here), then one lookup pair per thread
+        uint32_t *const late = reinterpret_cast<uint32_t *>(W.u.sim);
+        constexpr uint32_t LATE_CAP = WTILE;
+        if (tid == 0) W.v[9] = 0;
         __syncthreads();
-        for (uint32_t i = W.v[9] + tid; i < m; i += FILL_WG) {
-            const uint32_t c = cx(i);
-            if (!c || okey(kb(i)) < ksm) continue;
+        each_b<uint64_t>(nr, [&](uint32_t rr) { return ldc(&gs[rr]); }, [&](uint32_t, uint64_t s) {
+            const uint32_t c = rf_pos((uint32_t)s);
+            if ((uint32_t)(s >> 32) > dmx || !c || c < late_lo) return;
+            const uint32_t x = atomicAdd(&W.v[9], 1u);
+            if (x < LATE_CAP) late[x] = c;
+        });
+        __syncthreads();
+        const uint32_t nlate = uni(W.v[9]);
+        if (nlate > LATE_CAP) { O.why = 7; return O; }
+        for (uint32_t x = tid; x < nlate; x += FILL_WG) {
+            const uint32_t c = late[x];
             const uint32_t par = (c - 1u) / 2u, sib = ((c - 1u) ^ 1u) + 1u;
-            if (member(par) || (sib < I.N && member(sib))) {
+            if (member(par) || (sib < NN && member(sib))) {
                 const uint32_t q = c + 1u, dq = depth_of(q);
                 add_root(dq >= WHL ? (q >> WHL) - 1u : 0u);
             }
         }
         __syncthreads();
-        const uint32_t nroot = W.v[8];
+        LEAD_SUB(4);
+        const uint32_t nroot = uni(W.v[8]);
+        if (STG_CREW_STAMPS && tid == 0) I.dbg[5] = nroot;
         if (nroot > WROOTS) { O.why = 5; return O; }
         if (nroot) {
-            const uint32_t Dm = depth_of(I.N);  // depth of the last position N - 1
+            const uint32_t Dm = depth_of(NN);  // depth of the last position N - 1
             // maximal roots only (drop one with an ancestor, or an equal one before it, in the list)
             bool keep = false;
             uint32_t my = 0;
@@ -383,8 +530,16 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
             __syncthreads();
             if (keep) W.roots[WROOTS - 1u - atomicAdd(&W.v[10], 1u)] = my;  // kept roots at the end
             __syncthreads();
-            const uint32_t nk = W.v[10];
-            each_b<uint32_t>(m, cx, [&](uint32_t i, uint32_t c) { st_sc1(&gp[i], c); });  // positions: starts, then replays
+            const uint32_t nk = uni(W.v[10]);
+            // positions: starts, then replays
+            each_b<u4v>(nq, [&](uint32_t q) { return ld4(rc, q); }, [&](uint32_t q, u4v x) {
+                const uint32_t i = 4u * q;
+                st_sc1(&gp[i], x.x);
+                if (i + 1u < n) st_sc1(&gp[i + 1u], x.y);
+                if (i + 2u < n) st_sc1(&gp[i + 2u], x.z);
+                if (i + 3u < n) st_sc1(&gp[i + 3u], x.w);
+            });
+            if (tail && tid == 0) st_sc1(&gp[n], NN - 1u);
             vm_drain();
             __syncthreads();
             uint32_t late_bad = 0;
@@ -394,8 +549,8 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                 uint2 *const sim = W.u.sim;
                 for (uint32_t l = tid; l < nn; l += FILL_WG) sim[l] = make_uint2(0u, NONE);
                 if (tid <= h) {  // the list entries at each depth of the subtree
-                    const uint32_t lo = (qa << tid) - 1u, hi = min(lo + (1u << tid), I.N);
-                    const uint32_t f = lo < I.N ? lower(lo) : m, e = lo < I.N ? lower(hi) : m;
+                    const uint32_t lo = (qa << tid) - 1u, hi = min(lo + (1u << tid), NN);
+                    const uint32_t f = lo < NN ? lower(lo).x : m, e = lo < NN ? lower(hi).x : m;
                     W.lvl[tid] = f;
                     W.lvl[WHMAX + 2u + tid] = e - f;
                 }
@@ -406,14 +561,18 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                     W.v[11] = acc;
                 }
                 __syncthreads();
-                const uint32_t tot = W.v[11];
-                for (uint32_t f = tid; f < tot; f += FILL_WG) {
-                    uint32_t t = 0;
+                const uint32_t tot = uni(W.v[11]);
+                auto entry = [&](uint32_t f, uint32_t &t) {
+                    t = 0;
                     while (t < h && W.lvl[WHMAX + 3u + t] <= f) ++t;
-                    const uint32_t i = W.lvl[t] + (f - W.lvl[WHMAX + 2u + t]);
-                    const uint32_t k = okey(kb(i));
-                    if (k >= ksm) sim[(1u << t) - 1u + (cx(i) + 1u - (qa << t))] = make_uint2(k, i);
-                }
+                    return W.lvl[t] + (f - W.lvl[WHMAX + 2u + t]);
+                };
+                each_b<uint2>(tot, [&](uint32_t f) { uint32_t t; const uint32_t i = entry(f, t); return make_uint2(kb(i), cx(i)); },
+                              [&](uint32_t f, uint2 x) {
+                                  uint32_t t;
+                                  const uint32_t i = entry(f, t), k = okey(x.x);
+                                  if (k >= ksm) sim[(1u << t) - 1u + (x.y + 1u - (qa << t))] = make_uint2(k, i);
+                              });
                 __syncthreads();
                 // make_heap on the subtree: every node p <= (N - 2) / 2, deepest first,
                 // libstdc++'s __adjust_heap / __push_heap with len = N (non-R_smin: -inf = 0)
@@ -421,10 +580,10 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                     const uint32_t l0 = (1u << t) - 1u, w = 1u << t;
                     for (uint32_t o = tid; o < w; o += FILL_WG) {
                         const uint32_t top = (qa << t) - 1u + o;
-                        if (I.N < 2u || top > (I.N - 2u) / 2u) continue;
+                        if (NN < 2u || top > (NN - 2u) / 2u) continue;
                         const uint2 value = sim[l0 + o];
                         uint32_t hp = top, hl = l0 + o, sc = top;
-                        while (sc < (I.N - 1u) / 2u) {
+                        while (sc < (NN - 1u) / 2u) {
                             sc = 2u * (sc + 1u);
                             uint32_t cl = 2u * hl + 2u;
                             if (sim[cl].x < sim[cl - 1u].x) { --sc; --cl; }
@@ -432,7 +591,7 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                             hp = sc;
                             hl = cl;
                         }
-                        if ((I.N & 1u) == 0 && sc == (I.N - 2u) / 2u) {
+                        if ((NN & 1u) == 0 && sc == (NN - 2u) / 2u) {
                             sc = 2u * (sc + 1u);
                             sim[hl] = sim[2u * hl + 1u];
                             hp = sc - 1u;
@@ -458,51 +617,63 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                 __syncthreads();
             }
             if (__syncthreads_or((int)late_bad)) { O.why = 7; return O; }
-            // re-order every run by the replayed positions (rf32), through op
-            uint32_t big = 0;
-            for (uint32_t rr = tid; rr < nr; rr += FILL_WG) {
-                const uint32_t o = ld_sc1(&go[rr]);
-                if (!(o >> 31)) continue;
-                const uint32_t e = o & LNONE, k = okey(kb(e)), ke = rf32(ld_sc1(&gp[e]));
-                uint32_t g0 = rr, g1 = rr + 1u;
-                while (g0 > 0 && rr - g0 < WRUN && okey(kb(ld_sc1(&go[g0 - 1u]) & LNONE)) == k) --g0;
-                while (g1 < nr && g1 - rr < WRUN && okey(kb(ld_sc1(&go[g1]) & LNONE)) == k) ++g1;
-                if (g1 - g0 >= WRUN) { big = 1; continue; }
-                uint32_t rk = g0;
-                for (uint32_t x = g0; x < g1; ++x) rk += rf32(ld_sc1(&gp[ld_sc1(&go[x]) & LNONE])) < ke;
-                st_sc1(&op[rk], o);
+            LEAD_SUB(5);
+            // re-order every run by the replayed positions (rf32), one LDS tile
+            // of whole runs at a time
+            uint32_t *const dd = W.u.s.hist, *const rfk = W.u.s.hist + WTILE, *const oo = W.u.s.ti;
+            for (uint32_t s0 = 0; s0 < nr;) {
+                const uint32_t nt = min(WTILE, nr - s0), ext = s0 + nt < nr ? 1u : 0u;
+                each_b<uint2>(nt, [&](uint32_t j) { return make_uint2(ldc(&go[s0 + j]), ldc(&gs32[2u * (s0 + j) + 1u])); },
+                              [&](uint32_t j, uint2 x) { oo[j] = x.x; dd[j] = x.y; });
+                if (tid == 0) W.v[11] = ext ? ldc(&gs32[2u * (s0 + nt) + 1u]) : NONE;
+                __syncthreads();
+                each_b<uint32_t>(nt, [&](uint32_t j) { return ldc(&gp[oo[j] & LNONE]); },
+                                 [&](uint32_t j, uint32_t p) { rfk[j] = rf32(p); });
+                if (tid == 0) {  // the tile ends where a run ends
+                    uint32_t c = nt;
+                    if (ext) while (c > 0 && dd[c - 1u] == W.v[11]) --c;
+                    W.v[12] = c;
+                }
+                __syncthreads();
+                const uint32_t cut = uni(W.v[12]);
+                uint32_t big = cut == 0 ? 1u : 0u;
+                for (uint32_t j = tid; j < cut; j += FILL_WG) {
+                    const uint32_t o = oo[j];
+                    if (!(o >> 31)) continue;
+                    const uint32_t dj = dd[j], kj = rfk[j];
+                    uint32_t g0 = j, g1 = j + 1u;
+                    while (g0 > 0 && j - g0 < WRUN && dd[g0 - 1u] == dj) --g0;
+                    while (g1 < cut && g1 - j < WRUN && dd[g1] == dj) ++g1;
+                    if (g1 - g0 >= WRUN) { big = 1; continue; }
+                    uint32_t rk = g0;
+                    for (uint32_t x = g0; x < g1; ++x) rk += rfk[x] < kj;
+                    st_sc1(&go[s0 + rk], o);
+                }
+                vm_drain();
+                if (__syncthreads_or((int)big)) { O.why = 8; return O; }
+                s0 += cut;
             }
-            vm_drain();
-            if (__syncthreads_or((int)big)) { O.why = 8; return O; }
-            for (uint32_t rr = tid; rr < nr; rr += FILL_WG) {
-                const uint32_t o = ld_sc1(&go[rr]);
-                if (o >> 31) st_sc1(&go[rr], ld_sc1(&op[rr]));
-            }
-            vm_drain();
-            __syncthreads();
         }
     }
 
     // ---- 4. the pops: P and the ragged tail's rank; the order's positions ----
+    LEAD_STAMP(3);
     if (tid == 0) W.v[12] = NONE;
     __syncthreads();
-    if (I.tail)
-        each_b<uint32_t>(nr, [&](uint32_t rr) { return ld_sc1(&go[rr]); }, [&](uint32_t rr, uint32_t o) {
-            if ((o & LNONE) == I.n) W.v[12] = rr;
+    if (tail)
+        each_b<uint32_t>(nr, [&](uint32_t rr) { return ldc(&go[rr]); }, [&](uint32_t rr, uint32_t o) {
+            if ((o & LNONE) == n) W.v[12] = rr;
         });
     __syncthreads();
-    const uint32_t tr = W.v[12];
+    const uint32_t tr = uni(W.v[12]);
     uint32_t P = P0;
-    if (tr < P0) P = (I.rem + (16u - I.tl) + 15u) / 16u;
+    if (tr < P0) P = (uni(I.rem) + (16u - uni(I.tl)) + 15u) / 16u;
     if (P > nr) { O.why = 4; return O; }
-    each_b<uint32_t>(P, [&](uint32_t i) { return ld_sc1(&go[i]) & LNONE; }, [&](uint32_t i, uint32_t o) {
-        op[i] = o;  // the entries first (one round trip), their positions below
-    });
+    each_b2<uint32_t, uint32_t>(P, [&](uint32_t i) { return ldc(&go[i]) & LNONE; }, [&](uint32_t, uint32_t e) { return ps(e); },
+                                [&](uint32_t i, uint32_t, uint32_t p) { st_sc1(&op[i], p); });
     vm_drain();
     __syncthreads();
-    each_b<uint32_t>(P, [&](uint32_t i) { return ps(op[i]); }, [&](uint32_t i, uint32_t x) { st_sc1(&op[i], x); });
-    vm_drain();
-    __syncthreads();
+    LEAD_STAMP(4);
     O.P = P;
     O.tail_rank = tr;
     O.ordpos = op;
@@ -521,7 +692,7 @@ __device__ __forceinline__ bool crew_wants(uint32_t flags, uint32_t M, uint32_t 
 
 // scratch layout of a crew bucket (words of d.heap: 2 (nb + 64) of them)
 struct CrewMap {
-    uint32_t *keys, *qual, *lk, *lp, *lc;
+    uint32_t *keys, *lk, *lp, *lc;
     uint64_t *cdesc;
     uint32_t kwords, lcap;
 };
@@ -530,14 +701,13 @@ struct CrewMap {
 __device__ __forceinline__ CrewMap crew_map(const CrewBk &B) {
     CrewMap c;
     uint32_t *const g = uni_ptr(reinterpret_cast<uint32_t *>(B.d.heap));
-    const uint32_t nb = uni(B.d.nb), nA = uni(B.nA), nC = uni(B.nC);
+    const uint32_t nb = uni(B.d.nb), nC = uni(B.nC);
     const uint32_t total = 2u * (nb + 64u);
     c.kwords = (nb + 16u + 3u) & ~3u;
     c.keys = g;
-    c.qual = g + c.kwords;
-    const uint32_t co = (c.kwords + nA + 1u) & ~1u;
+    const uint32_t co = c.kwords;
     c.cdesc = reinterpret_cast<uint64_t *>(g + co);
-    const uint32_t lo = co + 2u * nC;
+    const uint32_t lo = (co + 2u * nC + 3u) & ~3u;
     c.lcap = total > lo ? (total - lo) / 3u : 0u;
     c.lk = g + lo;
     c.lp = c.lk + c.lcap;
@@ -545,7 +715,7 @@ __device__ __forceinline__ CrewMap crew_map(const CrewBk &B) {
     return c;
 }
 
-// A: one unit of 4,096 lines.
+// A: one unit of la lines.
 __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, uint32_t u) {
     u = uni(u);  // (a callee's arguments arrive in VGPRs)
     ctl = uni_ptr(ctl);
@@ -555,7 +725,7 @@ __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
     for (uint32_t b = tid; b < WBINS; b += FILL_WG) hist[b] = 0;
     __syncthreads();
     const uint32_t nb = uni(B.d.nb);
-    const uint32_t L0 = u * CW_LA, nl = nb > L0 ? min(CW_LA, nb - L0) : 0u;
+    const uint32_t la = uni(B.la), L0 = u * la, nl = nb > L0 ? min(la, nb - L0) : 0u;
     const float *const src = uni_ptr(B.d.src);
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(src + (size_t)L0 * 16), 0, nl * 64u, 0x00020000);
@@ -572,7 +742,6 @@ __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
     float4 v[CW_DA];
 #pragma unroll
     for (uint32_t j = 0; j < CW_DA; ++j) v[j] = load(j);
-    uint32_t nq = 0;
     for (uint32_t m0 = 0; m0 < mine; m0 += CW_DA) {
 #pragma unroll
         for (uint32_t j = 0; j < CW_DA; ++j) {
@@ -584,65 +753,73 @@ __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
             const bool valid = line < nl;
             const bool qual = S >= t;
             const uint32_t k = qual ? 0u : okey(f2u(S));
-            if (valid && !qual && q == 0) atomicAdd(&hist[k >> WSH], 1u);
-            nq += (valid && qual && q == 0) ? 1u : 0u;
+            if (STG_CREW_STAMPS != 4 && valid && !qual && q == 0) atomicAdd(&hist[k >> WSH], 1u);
             // lane 16 j stores the keys of lines 4 j .. 4 j + 3 of the step (one 16-byte sc1 store)
             const uint32_t k1 = __shfl_down(k, 4, 64), k2 = __shfl_down(k, 8, 64), k3 = __shfl_down(k, 12, 64);
-            if ((lane & 15u) == 0 && valid) {
+            if (STG_CREW_STAMPS != 3 && (lane & 15u) == 0 && valid) {
                 u4v kv;
                 kv.x = k; kv.y = k1; kv.z = k2; kv.w = k3;
                 __builtin_amdgcn_raw_buffer_store_b128(kv, rk, (L0 + s * 16u + (lane >> 2)) * 4u, 0, 16 /* sc1 */);
             }
         }
     }
-    nq = wave_sum(nq);
-    if (lane == 0) atomicAdd(&W.v[13], nq);  // zeroed by the caller
     if (u + 1u == uni(B.nA) && B.tail && tid == 0) atomicAdd(&hist[okey(B.tail_bits) >> WSH], 1u);
     __syncthreads();
     for (uint32_t b = tid; b < WBINS; b += FILL_WG) {
         const uint32_t c = hist[b];
         if (c) __hip_atomic_fetch_add(gp(&ctl->hist[b]), c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (tid == 0) st_sc1(&cm.qual[u], W.v[13]);
 }
 
-// B: the level-1 bin of the (sel + 1)-th largest candidate key.
-__device__ __noinline__ void crew_b(WideLds &W, const CrewBk &B, CrewCtl *ctl) {
-    ctl = uni_ptr(ctl);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t P0 = (B.rem + 15u) / 16u, sel = min(P0 + 1u, B.N - 1u);
-    constexpr uint32_t PER = WBINS / FILL_WG;
-    uint32_t c[PER], s = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        c[j] = ld_sc1(&ctl->hist[WBINS - 1u - (PER * tid + j)]);
-        s += c[j];
-    }
-    if (tid == 0) W.v[0] = 0;
-    uint32_t tot;
-    uint32_t a = blk_excl_scan<FNW_F>(s, W.sh, &tot);
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        if (a <= sel && sel < a + c[j]) W.v[0] = WBINS - 1u - (PER * tid + j);
-        a += c[j];
-    }
-    __syncthreads();
-    if (tid == 0) st_sc1(&ctl->beta, W.v[0]);
-}
-
-// C: list the candidates of bins >= beta in keys [c * LC, ...), in scan order.
+// C: the level-1 bin beta of the (sel + 1)-th largest candidate key (every
+// unit picks it from the bucket's histogram), then the candidates of bins >=
+// beta in keys [c * LC, ...), listed in scan order.
 __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, uint32_t c, uint32_t epoch) {
     c = uni(c);
     epoch = uni(epoch);
     ctl = uni_ptr(ctl);
-    const uint32_t tid = threadIdx.x, lane = tid & 63u;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const CrewMap cm = crew_map(B);
-    const uint32_t beta = uni(ld_sc1(&ctl->beta)), nb = uni(B.d.nb);
-    const uint32_t K0 = c * CW_LC + 32u * tid;
+    const uint32_t nb = uni(B.d.nb);
+    const uint32_t K0 = c * CW_LC + 16u * tid;
     const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(cm.keys, 0, nb * 4u, 0x00020000);
-    u4v kv[8];
+    u4v kv[4];
 #pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) kv[j] = __builtin_amdgcn_raw_buffer_load_b128(rk, (K0 + 4u * j) * 4u, 0, 16 /* sc1 */);
+    for (uint32_t j = 0; j < 4; ++j) kv[j] = __builtin_amdgcn_raw_buffer_load_b128(rk, (K0 + 4u * j) * 4u, 0, 16 /* sc1 */);
+    {   // the histogram into LDS beside them (8,192 words: 32 chunks of 64 lanes x 16 bytes)
+        const char *const src = reinterpret_cast<const char *>(ctl->hist);
+        char *const dst = reinterpret_cast<char *>(W.u.s.hist);
+        for (uint32_t ch = wave; ch < WBINS / 256u; ch += FNW_F)
+            __builtin_amdgcn_global_load_lds(src + (size_t)(ch * 64u + lane) * 16u, dst + ch * 1024u, 16, 0, 16 /* sc1 */);
+    }
+    vm_drain();
+    __syncthreads();
+    uint32_t beta, r1;
+    {   // descending bins, 16 per thread
+        const uint32_t P0 = (B.rem + 15u) / 16u, sel = min(P0 + 1u, B.N - 1u);
+        constexpr uint32_t PER = WBINS / FILL_WG;
+        uint32_t hc[PER], s = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) {
+            hc[j] = W.u.s.hist[WBINS - 1u - (PER * tid + j)];
+            s += hc[j];
+        }
+        if (tid == 0) { W.v[0] = 0; W.v[1] = 0; }
+        uint32_t tot;
+        uint32_t a = blk_excl_scan<FNW_F>(s, W.sh, &tot);
+#pragma unroll
+        for (uint32_t j = 0; j < PER; ++j) {
+            if (a <= sel && sel < a + hc[j]) { W.v[0] = WBINS - 1u - (PER * tid + j); W.v[1] = sel - a; }
+            a += hc[j];
+        }
+        __syncthreads();
+        beta = uni(W.v[0]);
+        r1 = uni(W.v[1]);
+    }
+    if (c == 0 && tid == 0) {
+        st_sc1(&ctl->beta, beta);
+        st_sc1(&ctl->pad[0], r1);  // its rank inside the bin (the leader starts there)
+    }
     auto key = [&](uint32_t j) -> uint32_t {
         const u4v x = kv[j >> 2];
         const uint32_t w = j & 3u;
@@ -650,7 +827,7 @@ __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
     };
     uint32_t nl = 0, nq = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 32; ++j) {
+    for (uint32_t j = 0; j < 16; ++j) {
         const uint32_t k = key(j);
         const bool in = K0 + j < nb;
         nq += (in && k == 0) ? 1u : 0u;
@@ -659,8 +836,9 @@ __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
     uint32_t NL, NQ;
     const uint32_t lo = blk_excl_scan<FNW_F>(nl, W.sh, &NL);
     const uint32_t qo = blk_excl_scan<FNW_F>(nq, W.sh, &NQ);
-    if (tid == 0) st_sc1(&cm.cdesc[c], ((uint64_t)epoch << 32) | NL);
-    if (tid < 64) {  // earlier units' counts (tagged, look-back) and the A units' qualifying lines before this unit
+    // {tag | qualifying lines : 16 | listed : 16} of this unit
+    if (tid == 0) st_sc1(&cm.cdesc[c], ((uint64_t)epoch << 32) | (NQ << 16) | NL);
+    if (tid < 64) {  // earlier units' counts (tagged, look-back)
         uint32_t sl = 0, sq = 0, ok = 1;
         for (uint32_t i = lane; i < c; i += 64u) {
             uint64_t x = ld_sc1(&cm.cdesc[i]);
@@ -670,28 +848,32 @@ __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
                 x = ld_sc1(&cm.cdesc[i]);
                 if (spin_expired(sp, st)) { ok = 0; break; }
             }
-            sl += (uint32_t)x;
+            sl += (uint32_t)x & 0xffffu;
+            sq += ((uint32_t)x >> 16) & 0xffffu;
         }
-        const uint32_t na = c * (CW_LC / CW_LA);
-        for (uint32_t i = lane; i < na; i += 64u) sq += ld_sc1(&cm.qual[i]);
         sl = wave_sum(sl);
         sq = wave_sum(sq);
         ok = __ballot(!ok) ? 0u : 1u;
-        if (lane == 0) { W.v[0] = sl; W.v[1] = sq; W.v[2] = ok; }
+        if (lane == 0) { W.v[2] = sl; W.v[3] = sq; W.v[4] = ok; }
     }
     __syncthreads();
-    if (!W.v[2]) return false;
-    uint32_t off = W.v[0] + lo, qb = W.v[1] + qo, ovf = 0;
+    if (!W.v[4]) return false;
+    uint32_t off = W.v[2] + lo, qb = W.v[3] + qo, ovf = 0;
+    // (buffer stores: a base in SGPRs and 32-bit offsets, sc1)
+    const __amdgpu_buffer_rsrc_t rlk = __builtin_amdgcn_make_buffer_rsrc(cm.lk, 0, cm.lcap * 4u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rlp = __builtin_amdgcn_make_buffer_rsrc(cm.lp, 0, cm.lcap * 4u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rlc = __builtin_amdgcn_make_buffer_rsrc(cm.lc, 0, cm.lcap * 4u, 0x00020000);
 #pragma unroll
-    for (uint32_t j = 0; j < 32; ++j) {
+    for (uint32_t j = 0; j < 16; ++j) {
         const uint32_t k = key(j), line = K0 + j;
         const bool in = line < nb;
         if (in && k == 0) ++qb;
         if (in && k && (k >> WSH) >= beta) {
             if (off < cm.lcap) {
-                st_sc1(&cm.lk[off], k & 0x7fffffffu);  // sums are >= +0: the ordered key is bits | 2^31
-                st_sc1(&cm.lp[off], line * 16u);
-                st_sc1(&cm.lc[off], line - qb);
+                // sums are >= +0: the ordered key is bits | 2^31
+                __builtin_amdgcn_raw_buffer_store_b32(k & 0x7fffffffu, rlk, off * 4u, 0, 16 /* sc1 */);
+                __builtin_amdgcn_raw_buffer_store_b32(line * 16u, rlp, off * 4u, 0, 16 /* sc1 */);
+                __builtin_amdgcn_raw_buffer_store_b32(line - qb, rlc, off * 4u, 0, 16 /* sc1 */);
             } else {
                 ovf = 1;
             }
@@ -699,7 +881,7 @@ __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
         }
     }
     if (__syncthreads_or((int)ovf) && tid == 0) st_sc1(&ctl->status, 1u);
-    if (c + 1u == B.nC && tid == 0) st_sc1(&ctl->nL, W.v[0] + NL);
+    if (c + 1u == B.nC && tid == 0) st_sc1(&ctl->nL, W.v[2] + NL);
     return true;
 }
 
@@ -713,13 +895,13 @@ struct CrewArgs {
     uint32_t epoch;
 };
 __device__ __forceinline__ uint32_t phase_units(const CrewBk &B, uint32_t p) {
-    return p == 1 ? B.nA : p == 3 ? B.nC : p == 5 ? CW_NE : 1u;
+    return p == 1 ? B.nA : p == 2 ? B.nC : p == 4 ? CW_NE : 1u;
 }
 
 __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A) {
     const uint32_t tid = threadIdx.x;
     CallCtl *const cc = A.cc;
-    uint32_t *const ticket = &cc->pad[6], *const done = &cc->pad[7];  // zeroed for each call by the scan
+    uint32_t *const ticket = &cc->crew_ticket[0], *const done = &cc->crew_done[0];  // zeroed for each call by the scan
     const uint32_t nreq = W.nreq;
     auto poison = [&]() {
         if (tid == 0) {
@@ -727,6 +909,7 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
             for (uint32_t j = 0; j < nreq; ++j) st_sc1(W.bk[j].d.count_out, POISON_COUNT);
         }
     };
+    if (STG_CREW_STAMPS && tid == 0) atomicMax(&A.dbg[23], (uint32_t)__builtin_amdgcn_s_memrealtime());  // the last crew start
     for (;;) {
         if (tid == 0) W.v[15] = g_add(ticket, 1u);
         __syncthreads();
@@ -748,14 +931,10 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
                 st_sc1_zero16(ctl->hist, WBINS * 4u, 16u * i);
             if (tid == 0) st_sc1(&ctl->status, 0u);
         } else if (p == 1) {  // A
-            if (tid == 0) W.v[13] = 0;
-            __syncthreads();
             crew_a(W, B, ctl, rel);
-        } else if (p == 2) {  // B
-            crew_b(W, B, ctl);
-        } else if (p == 3) {  // C
+        } else if (p == 2) {  // C
             if (!crew_c(W, B, ctl, rel, A.epoch)) { poison(); return; }
-        } else if (p == 4) {  // D: the leader, or the literal heap
+        } else if (p == 3) {  // D: the leader, or the literal heap
             const CrewMap cm = crew_map(B);
             const uint32_t nL = ld_sc1(&ctl->nL), ovf = ld_sc1(&ctl->status), beta = ld_sc1(&ctl->beta);
             LeadIn I;
@@ -771,10 +950,19 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
             I.tl = B.d.tl;
             I.g = cm.keys;  // the keys are dead once the list is built
             I.gcap = cm.kwords;
+            I.dbg = A.dbg;
+            I.lvl1 = beta;
+            I.r1 = ld_sc1(&ctl->pad[0]);
+            if (STG_CREW_STAMPS && tid == 0) A.dbg[29] = (uint32_t)__builtin_amdgcn_s_memrealtime();
             LeadOut O;
             O.ok = false;
             O.tail_rank = NONE;
             O.ordpos = cm.keys;
+            if (STG_CREW_STAMPS >= 2 && !ovf) {  // diagnostics: a first run warms the caches
+                (void)leader(W, I);
+                __syncthreads();
+                if (tid == 0) A.dbg[29] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            }
             if (!ovf) O = leader(W, I);
             const bool ok = O.ok;
             if (tid == 0) {
@@ -808,12 +996,14 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
 }
 
 // Units and tickets of the requested buckets (W.bk[0 .. nreq) filled).
-__device__ __forceinline__ void crew_plan(WideLds &W) {
+// A's units: the bucket's lines over the crew (at least CW_LA lines each).
+__device__ __forceinline__ void crew_plan(WideLds &W, uint32_t ncrew) {
     if (threadIdx.x == 0) {
         uint32_t t = 0;
         for (uint32_t j = 0; j < W.nreq; ++j) {
             CrewBk &B = W.bk[j];
-            B.nA = max(1u, (B.d.nb + CW_LA - 1u) / CW_LA);
+            B.la = max(CW_LA, ((B.d.nb + ncrew - 1u) / max(ncrew, 1u) + 255u) & ~255u);
+            B.nA = max(1u, (B.d.nb + B.la - 1u) / B.la);
             B.nC = max(1u, (B.d.nb + CW_LC - 1u) / CW_LC);
             W.tb[j] = t;
             for (uint32_t p = 0; p < CW_PH; ++p) {
@@ -854,7 +1044,7 @@ __device__ __forceinline__ void crew_from_decisions(WideLds &W, FillLds &S, cons
     }
     __syncthreads();
     if (!W.nreq) return;
-    crew_plan(W);
+    crew_plan(W, A.crew);
     crew_loop(W, S, CrewArgs{A.cc, A.fail, A.dbg, A.crew_ctl, A.epoch});
 }
 
@@ -884,6 +1074,6 @@ __device__ __forceinline__ void crew_lfin(LfinLds &Lf, const Tv16FillArgs &A) {
     }
     __syncthreads();
     if (!W.nreq) return;
-    crew_plan(W);
+    crew_plan(W, A.crew);
     crew_loop(W, *reinterpret_cast<FillLds *>(&Lf), CrewArgs{A.cc, A.fail, A.dbg, A.crew_ctl, A.epoch});
 }

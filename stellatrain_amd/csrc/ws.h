@@ -35,6 +35,8 @@ constexpr uint32_t TV16_CHUNK = 2048;        // lines (16 floats) per chunk = 12
 struct CallCtl {
     uint32_t next;      // dynamic chunk counter
     uint32_t pad[31];
+    uint32_t crew_ticket[32];  // the crew's ticket (its own line: taken by every crew workgroup)
+    uint32_t crew_done[32];    // the crew's completed units per phase (polled)
 };
 // Per-bucket regime decision, written by the finisher of the bucket's last
 // chunk: [1..3] first, drained, then [0] = {tag:32 | flags:32}; read by the
