@@ -59,7 +59,7 @@ for s in "$@"; do
             python3 tools/ktrace.py gpurun_out/prof_c5 24 > gpurun_out/prof_c5.txt 2>&1 ;;
         prof_merge) step prof_merge 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_merge" -o run -- python3 tools/bench_configs.py --only merge
             python3 tools/ktrace.py gpurun_out/prof_merge 16 > gpurun_out/prof_merge.txt 2>&1 ;;
-        scale_drop) step scale_drop 280 python tools/scale_drop.py 4 ;;
+        scale_drop) step scale_drop 280 python tools/scale_drop.py 4 ${DROPS:-100,10,2,1.1} ;;
         fill_paths) step fill_paths 200 python tools/fill_paths.py --steps 400 ;;
         stamps_r4) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_tk1st.so step tk1_stamps 150 python tools/tk1_stamps.py
             STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_crewst.so step crew_stamps 150 python tools/crew_stamps.py ;;
