@@ -111,7 +111,7 @@ struct Workspace {
         const size_t o_we = carve(sizeof(uint2) * stg::LNBIN * stg::LBCAP);
         const size_t o_crew = carve(sizeof(stg::CrewCtl) * stg::MAX_BATCH);
         const size_t o_tkc = carve(sizeof(stg::TopkCtl) * 2);
-        const size_t o_tkf = carve(sizeof(uint32_t) * stg::TK1_FINE);
+        const size_t o_tkf = carve(sizeof(uint32_t) * 2 * stg::TK2_FINE);
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
         // control block are ordered after it (a plain hipMemset runs on the

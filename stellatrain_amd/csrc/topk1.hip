@@ -1,5 +1,5 @@
-// topk1.hip -- Top-k by |x| in one launch, steered by the key's previous k-th
-// magnitude (gfx950).
+// topk1.hip -- Top-k by |x| in one pass over the bucket, steered by the key's
+// previous k-th magnitude (gfx950).
 //
 // Reference: TopkCompressor::impl_nth_element (compress/topk.cpp:28-46); the
 // two modes and their semantics are topk.hip's (the shipped byte-count memcpy
@@ -7,31 +7,32 @@
 // ties at the k-th magnitude T taken in index order.
 //
 // compress() carries the tensor's name (compressor.h:30), and a gradient's
-// magnitude distribution moves little from one iteration to the next, so the
-// key's last T (KeyState.t; the band's relative half width in KeyState.inc)
-// fixes a band [F, H) = T_prev (1 -/+ d) that almost always holds this call's
-// T.  Then one pass over the bucket replaces the select's passes:
-//   STREAM  per 32 KiB tile: its superset {|x| >= F} in index order, its count
-//           of keys >= H, the band's keys in a fine histogram (8,192 bins);
-//   PICK    (one workgroup) T's band bin and its rank inside the bin, from the
-//           histogram and the count above H -- or a miss;
-//   COUNT   per tile, from its superset: keys above T's bin; the bin's keys
-//           listed (a few per call);
-//   EXACT   (one workgroup) T from the list, the bin's keys into the per-tile
-//           (> T, == T) counts, their prefixes, the key's next hint;
-//   EMIT    per tile: the winners from its superset at their prefix offsets.
-// A band that misses T (or a key's first call) takes the select's way inside
-// the same launch -- three radix levels over the bucket (H1/P1, H2/P2,
-// H3/P3), per-tile counts (CNT, SCAN), EMIT re-reading the tiles -- and the
-// band doubles for the next call.
+// magnitude distribution moves little from one call to the next, so the key's
+// last T (KeyState.t; the band's relative half width d in KeyState.inc) fixes
+// a band [F, H) = T_prev (1 -/+ d), at most TK2_FINE ulps wide, that almost
+// always holds this call's T.  Two launches:
+//   tk2_stream  one workgroup per 32 KiB tile, no waits: the tile's superset
+//               {|x| >= F} (in index order) into region tile % 8 at an offset
+//               taken by one atomic; its count of keys >= H; every band key
+//               into the band histogram, one bin per ulp (and a coarse one per
+//               256 ulps).  One read of the bucket.
+//   tk_one      every workgroup finds T exactly from the histograms (the count
+//               above H, the coarse bins, one coarse bin's 256 ulps: T is a
+//               bin), then emission units of 16 tiles in ticket order count
+//               their supersets' (> T, == T) keys, publish them, sum the
+//               earlier units' (look-back) and write their winners in order.
+// A band that misses T, or a superset region that overflowed, takes the
+// select's way inside tk_one (three radix levels over the bucket, per-tile
+// counts, emission re-reading the tiles; units by sharded tickets, every
+// single-unit phase run by the workgroup that completes the phase before it)
+// and the band widens for the next call.  A key's first call runs topk.hip's
+// launches and seeds the hint (tk2_seed).
 //
-// Work goes by tickets, so no unit is waited on before a running workgroup
-// holds it: a multi-unit phase's tiles in 8 shards (tile % 8, each counter on
-// a line of its own), a workgroup draining its home shard (blockIdx % 8: one
-// XCD) and then the others; the workgroup whose unit completes a phase (the
-// last shard's last unit) runs the single-unit phase after it, the rest wait
-// for its flag, bounded.  Hand-offs are sc1 stores and loads, or device atomics.
+// No unit is waited on before a running workgroup holds it (tickets), and
+// every wait is bounded: a wait that gives up sets the failure word and
+// poisons the count.
 #include <algorithm>
+#include <cstdlib>
 
 #include "select.h"
 #include "tile.h"
@@ -41,7 +42,6 @@ namespace stg {
 
 namespace {
 
-using tv16::bitlen;
 using tv16::spin_expired;
 using tv16::vm_drain;
 
@@ -52,20 +52,160 @@ using tv16::vm_drain;
     do {                                                                                              \
         if (STG_TK1_STAMPS && threadIdx.x == 0) A.dbg[w] = (uint32_t)__builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// ... the latest over the workgroups
+#define TK1_STAMP_MAX(w)                                                                              \
+    do {                                                                                              \
+        if (STG_TK1_STAMPS && threadIdx.x == 0)                                                       \
+            atomicMax(&A.dbg[w], (uint32_t)__builtin_amdgcn_s_memrealtime());                         \
+    } while (0)
 
-constexpr uint32_t SUP_CAP1 = TOPK_SUP_CAP;
-constexpr uint32_t NB_BAND = TK1_FINE;
-constexpr uint32_t BINL = TK1_BINL;
-
-enum : uint32_t {
-    P_STREAM = 0, P_PICK, P_COUNT, P_EXACT,
-    M_H1, M_P1, M_H2, M_P2, M_H3, M_P3, M_CNT, M_SCAN,
-    P_EMIT, NPH
-};
+enum : uint32_t { M_H1 = 0, M_P1, M_H2, M_P2, M_H3, M_P3, M_CNT, M_SCAN, P_EMIT, NPH };
 static_assert(NPH == TK1_NPH, "phases");
+
+constexpr float D_MIN = 1.0f / 1024.0f;  // the band's relative half width d: narrowest
+constexpr float D_MAX = 1.0f / 128.0f;   // ... widest (2 d T_prev < TK2_FINE ulps)
+constexpr float D_SEED = 1.0f / 256.0f;  // ... after a key's first call
 
 __device__ __forceinline__ uint32_t mag1(uint32_t bits) { return bits & 0x7fffffffu; }
 
+// The band of this call from the key's hint: [F, H) in key bits, at most
+// TK2_FINE wide (centred on T_prev when d T_prev spans more ulps); ok = false
+// for a hint that cannot steer (zero, denormal, inf or NaN).
+struct Band {
+    uint32_t F, H;
+    bool ok;
+};
+__device__ __forceinline__ Band band_of(const KeyState *st) {
+    const float t = st->t, d = st->inc;
+    const uint32_t tb = mag1(f2u(t));
+    Band b;
+    b.ok = st->init && tb >= 0x00800000u && tb < 0x7f800000u;
+    b.F = mag1(f2u(t * (1.0f - d)));
+    b.H = mag1(f2u(t * (1.0f + d)));
+    if (b.H <= b.F) b.H = b.F + 1u;
+    if (b.H - b.F > TK2_FINE) {
+        b.F = tb - TK2_FINE / 2u;
+        b.H = b.F + TK2_FINE;
+    }
+    return b;
+}
+
+// ---------------------------------------------------------------------------
+// the stream launch
+// ---------------------------------------------------------------------------
+#ifndef STG_TK2_NOATOM
+#define STG_TK2_NOATOM 0  // experiment: no band histogram (results wrong)
+#endif
+#ifndef STG_TK2_FIXED
+#define STG_TK2_FIXED 0   // experiment: fixed per-tile superset slots instead of an offset atomic
+#endif
+struct T2Stream {
+    const float *a;
+    uint64_t m;
+    uint32_t last_mask, nt;
+    const KeyState *state;
+    TopkCtl *ctl;
+    uint32_t *fine;        // this call's band histogram (TK2_FINE words, zero)
+    uint2 *sup;            // superset regions: TK1_SH of shard_cap entries {element, bits}
+    uint32_t shard_cap;
+    uint32_t *sup_n, *sup_off;  // per tile: superset entries, offset in region tile % 8
+    uint32_t *count_out;
+    uint32_t cap;
+};
+
+template <bool VEC>
+__global__ void __launch_bounds__(STG_WG) tk2_stream(const T2Stream A) {
+    __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
+    __shared__ uint32_t s_off, s_hi;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, tile = blockIdx.x;
+    const Band B = band_of(A.state);
+    if (!B.ok) return;  // tk_one takes the select's way (band_ok stays 0)
+    if (tile == 0 && tid == 0) {
+        *A.count_out = A.cap;  // the band's way fills every slot; a failure in tk_one poisons it (atomicMax)
+        A.ctl->band_F = B.F;
+        A.ctl->band_H = B.H;
+        A.ctl->band_ok = 1u;
+    }
+    if (tid == 0) s_hi = 0;
+    const size_t base = (size_t)tile * TV_TILE, m = A.m;
+    float4 v[TILE_U];
+    load_tile<VEC>(A.a, m, base, A.last_mask, v);
+    uint32_t q = 0, pre[TILE_U], nhi = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < TILE_U; ++u) {
+        const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t key = mag1(f2u(comp(v[u], j)));
+            if (e + j < m && key >= B.F) {
+                q |= 1u << (u * 4 + j);
+                if (key >= B.H) {
+                    ++nhi;
+                } else if (!STG_TK2_NOATOM) {
+                    const uint32_t f = key - B.F;
+                    __hip_atomic_fetch_add(gp(&A.fine[f]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(gp(&A.ctl->coarse[f >> TK2_CSH]), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        const uint32_t c = (uint32_t)__popc((q >> (4 * u)) & 0xfu);
+        const uint32_t incl = wave_incl_scan(c);
+        pre[u] = incl - c;
+        if (lane == 63) s_wt[u * STG_WAVES + wave] = incl;
+    }
+    nhi = wave_sum(nhi);
+    __syncthreads();
+    if (lane == 0 && nhi) atomicAdd(&s_hi, nhi);
+    if (tid < 64) {  // (u, wave) offsets: one wave scans the 32 counts
+        constexpr uint32_t NW = TILE_U * STG_WAVES;
+        static_assert(NW <= 64, "one wave scans the wave counts");
+        const uint32_t x = tid < NW ? s_wt[tid] : 0u;
+        const uint32_t inc = wave_incl_scan(x);
+        if (tid < NW) s_wt[tid] = inc - x;
+        if (tid == NW - 1) s_wt[NW] = inc;
+    }
+    __syncthreads();
+    const uint32_t nsup = s_wt[TILE_U * STG_WAVES], sh = tile % TK1_SH;
+    if (tid == 0) {
+        uint32_t off = 0;
+        if (STG_TK2_FIXED) {
+            off = (tile / TK1_SH) * TOPK_SUP_CAP;
+            if (nsup > TOPK_SUP_CAP) { A.ctl->ovf = 1u; off = A.shard_cap; }
+        } else if (nsup) {
+            off = g_add(&A.ctl->shn[sh][0], nsup);
+            if (off + nsup > A.shard_cap) A.ctl->ovf = 1u;
+        }
+        s_off = off;
+        A.sup_n[tile] = nsup;
+        A.sup_off[tile] = off;
+        if (s_hi) g_add(&A.ctl->hi[tile % TK2_HI][0], s_hi);
+    }
+    __syncthreads();
+    const uint32_t off = s_off;
+    if (!nsup || off + nsup > A.shard_cap) return;
+    uint2 *const dst = A.sup + (size_t)sh * A.shard_cap + off;
+#pragma unroll
+    for (uint32_t u = 0; u < TILE_U; ++u) {
+        const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+        uint32_t slot = s_wt[u * STG_WAVES + wave] + pre[u];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((q >> (u * 4 + j)) & 1u) dst[slot++] = make_uint2((uint32_t)(e + j), f2u(comp(v[u], j)));
+    }
+}
+
+// A key's first call ran topk.hip's launches: T (rs->prefix) seeds the hint.
+__global__ void tk2_seed(KeyState *st, const RSel *rs, uint32_t *dbg) {
+    st->t = u2f(rs->prefix);
+    st->inc = D_SEED;
+    st->init = 1;
+    atomicAdd(&dbg[39], 1u);  // a call that took the select's way
+}
+
+// ---------------------------------------------------------------------------
+// the emission launch
+// ---------------------------------------------------------------------------
 struct T1Args {
     const float *a;
     uint64_t m, zeros;
@@ -77,169 +217,207 @@ struct T1Args {
     uint32_t *count_out;
     uint32_t *fail;
     KeyState *state;       // t: the previous call's T, inc: the band's relative half width, init: valid
-    bool hinted;           // the key has a T from an earlier call (its first call takes the select's way)
     TopkCtl *ctl, *ctl_next;
     uint32_t tag;          // >= 1
     RSel *rs;              // the select's way
-    uint2 *sup;            // per tile: superset {element, bits}, SUP_CAP1 entries
-    uint32_t *sup_n;       // per tile: superset size
-    uint32_t *sup_hi;      // per tile: keys >= H
-    uint32_t *tile_gt, *tile_eq;  // scan_tiles layout: counts [0, nt), prefixes [nt, 2nt), totals [2nt]
-    uint32_t *fine;        // band histogram (zero between calls)
+    const uint2 *sup;      // the stream launch's superset regions
+    uint32_t shard_cap;
+    const uint32_t *sup_n, *sup_off;
+    uint32_t *tile_gt, *tile_eq;  // the select's way: counts [0, nt), prefixes [nt, 2nt), totals [2nt]
+    const uint32_t *fine;  // this call's band histogram
+    uint32_t *fine_next;   // the next call's (zeroed here)
     uint32_t *dbg;         // ws.misc: [38] calls resolved in the band, [39] calls that took the select's way
+    uint32_t ut;           // tiles per emission unit (<= TK2_UT): about ER STG_WG superset entries
+    bool force_miss;       // tests (STG_TK1_DEBUG=2): the select's way every call
 };
+
+constexpr uint32_t ER = 8;  // superset entries per thread per emission round
 
 struct T1Lds {
     uint32_t s_wt[TILE_U * STG_WAVES + 1];
     uint32_t sh[STG_WAVES + 1];
-    union {
-        uint32_t h[2048];  // a select level's tile histogram
-        uint2 bl[BINL];    // EXACT: T's bin
-    } u;
+    uint64_t sh64[STG_WAVES];
+    uint32_t h[2048];       // a select level's tile histogram
+    uint32_t uc[TK2_UT], uo[TK2_UT], up[TK2_UT + 1], ub[TK2_UT];  // emission unit: per tile count, offset, flat start, base
     uint32_t v[16];
 };
 
 // shard s of a phase with U units holds units s, s + 8, ...
 __device__ __forceinline__ uint32_t shard_units(uint32_t U, uint32_t s) { return U > s ? (U - s + TK1_SH - 1) / TK1_SH : 0u; }
 
-// The band of this call from the key's hint.
-struct Band {
-    uint32_t F, H, sh;  // key bits: [F, H); fine bin = (key - F) >> sh
-};
-__device__ __forceinline__ Band band_of(const KeyState *st) {
-    const float t = st->t, d = st->inc;
-    Band b;
-    b.F = mag1(f2u(t * (1.0f - d)));
-    b.H = mag1(f2u(t * (1.0f + d)));
-    if (b.H <= b.F) b.H = b.F + 1u;
-    const uint32_t span = b.H - b.F;
-    b.sh = bitlen(span - 1u) > 13u ? bitlen(span - 1u) - 13u : 0u;
-    return b;
+__device__ __forceinline__ void t1_broken(const T1Args &A) {
+    g_or(A.fail, FAIL_SELECT);
+    __hip_atomic_fetch_max(gp(A.count_out), POISON_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---------------------------------------------------------------------------
-// multi-unit phase bodies (one tile each)
-// ---------------------------------------------------------------------------
-// STREAM: the tile's superset {|x| >= F} in index order (tk_pass's ranks), its
-// count of keys >= H, the band's keys into the fine histogram
-template <bool VEC>
-__device__ __noinline__ void unit_stream(const T1Args &A, T1Lds &L, uint32_t tile, const Band B) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const size_t base = (size_t)tile * TV_TILE;
-    const size_t m = A.m;
-    float4 v[TILE_U];
-    load_tile<VEC>(A.a, m, base, A.last_mask, v);
-    uint32_t q = 0, pre[TILE_U], nhi = 0;
-    uint32_t *const fine = A.fine;
+// T exactly from the stream launch's histograms, by every workgroup (a few
+// KiB from L2; no workgroup waits for another): the count above H, the coarse
+// bins top-down, then the 256 one-ulp bins of T's coarse bin.  Returns hit.
+struct Pick {
+    uint32_t T, gt;  // T; keys > T
+};
+__device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
+    const uint32_t tid = threadIdx.x;
+    const TopkCtl *const C = A.ctl;
+    // plain loads: written by the stream launch (a kernel boundary), read by
+    // every workgroup -- cached in each XCD's L2, where coherent (sc1) loads of
+    // the same few lines by 512 workgroups queue at the memory side
+    const uint32_t ok = C->band_ok, ovf = C->ovf, F = C->band_F;
+    constexpr uint32_t PER = TK2_COARSE / STG_WG;
+    uint32_t c[PER], s = 0, hi = tid < TK2_HI ? C->hi[tid][0] : 0u;
 #pragma unroll
-    for (uint32_t u = 0; u < TILE_U; ++u) {
-        const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+    for (uint32_t j = 0; j < PER; ++j) {  // top-down: thread tid holds coarse bins 1023 - (PER tid + j)
+        c[j] = C->coarse[TK2_COARSE - 1u - (PER * tid + j)];
+        s += c[j];
+    }
+    uint32_t th, tband;
+    (void)blk_excl_scan<STG_WAVES>(hi, L.sh, &th);
+    if (tid == 0) L.v[2] = 0xffffffffu;
+    uint32_t above = blk_excl_scan<STG_WAVES>(s, L.sh, &tband);
+    const uint32_t r = A.k - 1u;  // T's descending rank
+    const bool hit = ok && !ovf && th <= r && r - th < tband;
+    if (!__syncthreads_or((int)hit)) return false;  // (uniform)
+    const uint32_t rr = r - th;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t key = mag1(f2u(comp(v[u], j)));
-            if (e + j < m && key >= B.F) {
-                q |= 1u << (u * 4 + j);
-                if (key >= B.H) ++nhi;
-                else __hip_atomic_fetch_add(gp(&fine[(key - B.F) >> B.sh]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t j = 0; j < PER; ++j) {
+        if (above <= rr && rr < above + c[j]) { L.v[2] = TK2_COARSE - 1u - (PER * tid + j); L.v[3] = rr - above; }
+        above += c[j];
+    }
+    __syncthreads();
+    const uint32_t cb = L.v[2], rc = L.v[3];
+    const uint32_t f = A.fine[(cb << TK2_CSH) + (1u << TK2_CSH) - 1u - tid];  // top-down
+    static_assert((1u << TK2_CSH) == STG_WG, "one fine bin per thread");
+    if (tid == 0) L.v[4] = 0xffffffffu;
+    uint32_t tot;
+    const uint32_t fa = blk_excl_scan<STG_WAVES>(f, L.sh, &tot);
+    if (f && fa <= rc && rc < fa + f) { L.v[4] = (1u << TK2_CSH) - 1u - tid; L.v[5] = fa; }
+    __syncthreads();
+    if (L.v[4] == 0xffffffffu) return false;  // the bins disagree (cannot happen): the select's way
+    P.T = F + (cb << TK2_CSH) + L.v[4];
+    P.gt = th + (r - th - rc) + L.v[5];  // above H, the coarse bins above T's, T's bin's ulps above T
+    __syncthreads();
+    return true;
+}
+
+// One emission unit: tiles [u UT, u UT + UT).  Counts the (> T, == T) keys of
+// their supersets, publishes them, sums the earlier units' (look-back: units
+// are taken in ticket order, so each is held by a running or finished
+// workgroup) and writes the winners at their offsets.  Returns false when a
+// wait gave up.
+__device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, uint32_t T, uint64_t need_eq) {
+    const uint32_t tid = threadIdx.x, nt = A.nt;
+    const uint32_t UT = A.ut, t0 = u * UT, nT = std::min(UT, nt - t0);
+    if (tid < nT) {
+        L.uc[tid] = A.sup_n[t0 + tid];
+        L.uo[tid] = A.sup_off[t0 + tid];
+    }
+    __syncthreads();
+    if (tid < 64) {  // the tiles' flat starts: one wave scans the counts
+        const uint32_t c = tid < nT ? L.uc[tid] : 0u, o = tid < nT ? L.uo[tid] : 0u;
+        const uint32_t incl = wave_incl_scan(c), ex = incl - c;
+        const bool bad = tid < nT && (c > TV_TILE || o + c > A.shard_cap);
+        if (tid <= TK2_UT) L.up[tid] = tid < nT ? ex : 0xffffffffu;
+        // entry f of tile j is at sup[ub[j] + f] (mod 2^32: the true index is < 2^32)
+        if (tid < nT) L.ub[tid] = ((t0 + tid) % TK1_SH) * A.shard_cap + o - ex;
+        const uint32_t tot = __shfl(incl, (int)nT - 1, 64);
+        if (tid == nT) L.up[tid] = tot;
+        const uint64_t b = __ballot(bad);
+        if (tid == 0) L.v[11] = b ? 1u : 0u;
+    }
+    __syncthreads();
+    if (L.v[11]) {  // cannot happen: the stream launch wrote every tile's count and offset
+        if (tid == 0) t1_broken(A);
+        return true;
+    }
+    const uint32_t N = L.up[nT];
+    // the tiles' flat starts in scalar registers: entry f's tile is the count of
+    // starts (after the first) at or below f -- no branch, so a round's loads
+    // are all issued before any is waited for
+    uint32_t st1[TK2_UT - 1];
+#pragma unroll
+    for (uint32_t t = 1; t < TK2_UT; ++t) st1[t - 1] = tv16::uni(t < nT ? L.up[t] : 0xffffffffu);
+    auto ld = [&](uint32_t f) -> uint2 {
+        uint32_t j = 0;
+#pragma unroll
+        for (uint32_t t = 0; t + 1 < TK2_UT; ++t) j += st1[t] <= f ? 1u : 0u;
+        return A.sup[L.ub[j] + f];
+    };
+    uint2 e[ER];
+    auto load_round = [&](uint32_t b0) {
+#pragma unroll
+        for (uint32_t r = 0; r < ER; ++r) {
+            const uint32_t f = b0 + ER * tid + r;
+            e[r] = ld(std::min(f, N ? N - 1u : 0u));
+        }
+    };
+    // counts
+    uint32_t gt = 0, eq = 0;
+    for (uint32_t b0 = 0; b0 < N; b0 += ER * STG_WG) {
+        load_round(b0);
+#pragma unroll
+        for (uint32_t r = 0; r < ER; ++r) {
+            const uint32_t key = mag1(e[r].y);
+            const bool in = b0 + ER * tid + r < N;
+            gt += in && key > T;
+            eq += in && key == T;
+        }
+    }
+    uint32_t GT, EQ;
+    (void)blk_excl_scan<STG_WAVES>(gt, L.sh, &GT);
+    (void)blk_excl_scan<STG_WAVES>(eq, L.sh, &EQ);
+    TopkCtl *const C = A.ctl;
+    TK1_STAMP_MAX(46);  // the last unit counted
+    if (tid == 0) st_sc1(&C->udesc[u], ((uint64_t)(GT | 0x80000000u) << 32) | EQ);
+    // look-back: the earlier units' counts, one thread per unit
+    uint64_t pg = 0, pe = 0;
+    uint32_t bad = 0;
+    for (uint32_t i = tid; i < u; i += STG_WG) {
+        uint64_t w = ld_sc1(&C->udesc[i]);
+        uint64_t st = 0;
+        for (uint32_t sp = 0; !(w >> 63); ++sp) {
+            __builtin_amdgcn_s_sleep(2);
+            w = ld_sc1(&C->udesc[i]);
+            if (spin_expired(sp, st)) { bad = 1; break; }
+        }
+        pg += (w >> 32) & 0x7fffffffu;
+        pe += (uint32_t)w;
+    }
+    if (__syncthreads_or((int)bad)) return false;
+    TK1_STAMP_MAX(47);  // the last look-back done
+    const uint64_t gt_before = blk_sum64<STG_WAVES>(pg, L.sh64), eq_before = blk_sum64<STG_WAVES>(pe, L.sh64);
+    if (!(GT || (EQ && eq_before < need_eq))) return true;
+    // emission: > T always, == T in index order while fewer than need_eq came before
+    uint64_t wbase = gt_before + std::min(eq_before, need_eq), ebase = eq_before;
+    for (uint32_t b0 = 0; b0 < N; b0 += ER * STG_WG) {
+        if (N > ER * STG_WG) load_round(b0);  // (one round: still in registers)
+        uint32_t qg = 0, qe = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < ER; ++r) {
+            const uint32_t key = mag1(e[r].y);
+            const bool in = b0 + ER * tid + r < N;
+            qg |= (in && key > T) ? 1u << r : 0u;
+            qe |= (in && key == T) ? 1u << r : 0u;
+        }
+        uint32_t te, tw;
+        uint32_t er = blk_excl_scan<STG_WAVES>((uint32_t)__popc(qe), L.sh, &te);
+        uint32_t qw = qg;
+#pragma unroll
+        for (uint32_t r = 0; r < ER; ++r)
+            if ((qe >> r) & 1u) { if (ebase + er < need_eq) qw |= 1u << r; ++er; }
+        uint32_t wr = blk_excl_scan<STG_WAVES>((uint32_t)__popc(qw), L.sh, &tw);
+#pragma unroll
+        for (uint32_t r = 0; r < ER; ++r) {
+            if ((qw >> r) & 1u) {
+                const uint64_t slot = wbase + wr++;
+                if (slot >= A.k) { t1_broken(A); continue; }
+                A.idx[slot] = A.bug_compat ? (uint32_t)slot : e[r].x + (uint32_t)A.idx_offset;
+                A.val[slot] = u2f(e[r].y);
             }
         }
-        const uint32_t c = (uint32_t)__popc((q >> (4 * u)) & 0xfu);
-        const uint32_t incl = wave_incl_scan(c);
-        pre[u] = incl - c;
-        if (lane == 63) L.s_wt[u * STG_WAVES + wave] = incl;
+        wbase += tw;
+        ebase += te;
     }
-    nhi = wave_sum(nhi);
-    if (lane == 0) atomicAdd(&L.v[1], nhi);  // zeroed by the caller
-    __syncthreads();
-    if (tid < 64) {  // (u, wave) offsets: one wave scans the 32 counts
-        constexpr uint32_t NW = TILE_U * STG_WAVES;
-        static_assert(NW <= 64, "one wave scans the wave counts");
-        const uint32_t x = tid < NW ? L.s_wt[tid] : 0u;
-        const uint32_t inc = wave_incl_scan(x);
-        if (tid < NW) L.s_wt[tid] = inc - x;
-        if (tid == NW - 1) L.s_wt[NW] = inc;
-    }
-    __syncthreads();
-    const uint32_t nsup = L.s_wt[TILE_U * STG_WAVES];
-    if (nsup <= SUP_CAP1) {
-        uint64_t *const dst = reinterpret_cast<uint64_t *>(A.sup + (size_t)tile * SUP_CAP1);
-#pragma unroll
-        for (uint32_t u = 0; u < TILE_U; ++u) {
-            const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
-            uint32_t slot = L.s_wt[u * STG_WAVES + wave] + pre[u];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((q >> (u * 4 + j)) & 1u)
-                    st_sc1(dst + slot++, ((uint64_t)f2u(comp(v[u], j)) << 32) | (uint32_t)(e + j));
-        }
-    }
-    if (tid == 0) {
-        st_sc1(&A.sup_n[tile], nsup);
-        st_sc1(&A.sup_hi[tile], L.v[1]);
-    }
-}
-
-// The tile's keys (superset entries, or the tile re-read when it overflowed
-// its superset) >= lo, one at a time: f(element, bits).
-template <bool VEC, typename F>
-__device__ __forceinline__ void tile_keys(const T1Args &A, uint32_t tile, uint32_t lo, bool from_sup, F f) {
-    const uint32_t n = from_sup ? ld_sc1(&A.sup_n[tile]) : SUP_CAP1 + 1u;
-    if (n <= SUP_CAP1) {
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(A.sup + (size_t)tile * SUP_CAP1);
-        uint64_t w[4];
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t j = 4 * threadIdx.x + r;
-            w[r] = j < n ? ld_sc1(&src[j]) : 0ull;
-        }
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r)
-            if (4 * threadIdx.x + r < n) f((uint32_t)w[r], (uint32_t)(w[r] >> 32));
-        return;
-    }
-    const size_t base = (size_t)tile * TV_TILE;
-    float4 v[TILE_U];
-    load_tile<VEC>(A.a, A.m, base, A.last_mask, v);
-#pragma unroll
-    for (uint32_t u = 0; u < TILE_U; ++u) {
-        const size_t e = base + 4 * ((size_t)u * STG_WG + threadIdx.x);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (e + j < A.m && mag1(f2u(comp(v[u], j))) >= lo) f((uint32_t)(e + j), f2u(comp(v[u], j)));
-    }
-}
-
-// COUNT: the tile's keys above T's band bin [blo, bhi); the bin's keys listed
-template <bool VEC>
-__device__ __noinline__ void unit_countband(const T1Args &A, T1Lds &L, uint32_t tile, uint32_t blo, uint32_t bhi) {
-    const uint32_t tid = threadIdx.x;
-    uint32_t above = 0;
-    if (tid == 0) L.v[2] = 0;
-    __syncthreads();
-    tile_keys<VEC>(A, tile, blo, true, [&](uint32_t e, uint32_t bits) {
-        const uint32_t key = mag1(bits);
-        if (key >= bhi) ++above;
-        else if (key >= blo) {
-            const uint32_t x = atomicAdd(&L.v[2], 1u);
-            if (x < BINL) L.u.bl[x] = make_uint2(e, key);
-        }
-    });
-    uint32_t tot;
-    (void)blk_excl_scan<STG_WAVES>(above, L.sh, &tot);
-    const uint32_t nb = min(L.v[2], BINL);
-    if (tid == 0) {
-        st_sc1(&A.tile_gt[tile], tot);
-        st_sc1(&A.tile_eq[tile], 0u);
-        L.v[3] = nb ? g_add(&A.ctl->nbin_list, nb) : 0u;
-        if (L.v[2] > BINL) g_add(&A.ctl->nbin_list, BINL + 1u);  // a crowded bin: EXACT gives up
-    }
-    __syncthreads();
-    const uint32_t b0 = L.v[3];
-    for (uint32_t i = tid; i < nb; i += STG_WG)
-        if (b0 + i < BINL) {
-            const uint2 x = L.u.bl[i];
-            st_sc1(reinterpret_cast<uint64_t *>(A.ctl->binl) + b0 + i, ((uint64_t)x.y << 32) | x.x);
-        }
+    return true;
 }
 
 // A select level's histogram over one tile (the keys under the prefix).
@@ -247,7 +425,7 @@ template <bool VEC, int SHIFT, int NBITS>
 __device__ __noinline__ void unit_hist(const T1Args &A, T1Lds &L, uint32_t tile) {
     const uint32_t tid = threadIdx.x;
     constexpr uint32_t NB = 1u << NBITS;
-    for (uint32_t i = tid; i < NB; i += STG_WG) L.u.h[i] = 0;
+    for (uint32_t i = tid; i < NB; i += STG_WG) L.h[i] = 0;
     const uint32_t prefix = SHIFT == 20 ? 0u : ld_sc1(&A.rs->prefix), mask = SHIFT == 20 ? 0u : ld_sc1(&A.rs->mask);
     __syncthreads();
     const size_t base = (size_t)tile * TV_TILE;
@@ -259,12 +437,12 @@ __device__ __noinline__ void unit_hist(const T1Args &A, T1Lds &L, uint32_t tile)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t key = mag1(f2u(comp(v[u], j)));
-            if (e + j < A.m && (key & mask) == prefix) atomicAdd(&L.u.h[(key >> SHIFT) & (NB - 1u)], 1u);
+            if (e + j < A.m && (key & mask) == prefix) atomicAdd(&L.h[(key >> SHIFT) & (NB - 1u)], 1u);
         }
     }
     __syncthreads();
     for (uint32_t i = tid; i < NB; i += STG_WG)
-        if (L.u.h[i]) g_add(&A.rs->hist[tile % RS_SHARDS][i], L.u.h[i]);
+        if (L.h[i]) g_add(&A.rs->hist[tile % RS_SHARDS][i], L.h[i]);
 }
 
 // CNT: the tile's keys > T and == T (the select's way)
@@ -293,53 +471,15 @@ __device__ __noinline__ void unit_count(const T1Args &A, T1Lds &L, uint32_t tile
     }
 }
 
-__device__ __forceinline__ void t1_broken(const T1Args &A) {
-    g_or(A.fail, FAIL_SELECT);
-    st_sc1(A.count_out, POISON_COUNT);
-}
-
-// EMIT: the tile's winners (> T, then == T in index order until k) at their
-// prefix offsets: from the superset, or from the tile itself.
+// EMIT (the select's way): the tile's winners (> T, then == T in index order
+// until k) at their prefix offsets, from the tile itself.
 template <bool VEC>
-__device__ __noinline__ void unit_emit(const T1Args &A, T1Lds &L, uint32_t tile, uint32_t T, uint64_t need_eq,
-                                       bool from_sup) {
+__device__ __noinline__ void unit_emit(const T1Args &A, T1Lds &L, uint32_t tile, uint32_t T, uint64_t need_eq) {
     const uint32_t tid = threadIdx.x, nt = A.nt;
     const uint32_t cg = ld_sc1(&A.tile_gt[tile]), ce = ld_sc1(&A.tile_eq[tile]);
     const uint64_t gt_before = ld_sc1(&A.tile_gt[nt + tile]), eq_before = ld_sc1(&A.tile_eq[nt + tile]);
     if (!(cg || (ce && eq_before < need_eq))) return;
     const uint64_t win_before = gt_before + std::min(eq_before, need_eq);
-    const uint32_t n = from_sup ? ld_sc1(&A.sup_n[tile]) : SUP_CAP1 + 1u;
-    if (n <= SUP_CAP1) {
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(A.sup + (size_t)tile * SUP_CAP1);
-        uint2 x[4];
-        uint32_t qe = 0, qg = 0;
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t j = 4 * tid + r;
-            const uint64_t w = j < n ? ld_sc1(&src[j]) : 0ull;
-            x[r] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
-            const uint32_t key = mag1(x[r].y);
-            if (j < n && key > T) qg |= 1u << r;
-            if (j < n && key == T) qe |= 1u << r;
-        }
-        uint32_t tot;
-        uint32_t er = blk_excl_scan<STG_WAVES>((uint32_t)__popc(qe), L.sh, &tot);
-        uint32_t qw = qg;
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r)
-            if ((qe >> r) & 1u) { if (eq_before + er < need_eq) qw |= 1u << r; ++er; }
-        uint32_t wr = blk_excl_scan<STG_WAVES>((uint32_t)__popc(qw), L.sh, &tot);
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            if ((qw >> r) & 1u) {
-                const uint64_t slot = win_before + wr++;
-                if (slot >= A.k) { t1_broken(A); continue; }
-                A.idx[slot] = A.bug_compat ? (uint32_t)slot : x[r].x + (uint32_t)A.idx_offset;
-                A.val[slot] = u2f(x[r].y);
-            }
-        }
-        return;
-    }
     float4 v[TILE_U];
     const size_t base = (size_t)tile * TV_TILE;
     load_tile<VEC>(A.a, A.m, base, A.last_mask, v);
@@ -379,9 +519,6 @@ __device__ __noinline__ void unit_emit(const T1Args &A, T1Lds &L, uint32_t tile,
     }
 }
 
-// ---------------------------------------------------------------------------
-// single-unit phases (the workgroup that completed the phase before)
-// ---------------------------------------------------------------------------
 // topk.hip's scan_tiles with sc1 stores: its prefixes are read by other
 // workgroups of this launch (sc1 loads), not after a kernel boundary.
 __device__ __noinline__ void scan_tiles1(uint32_t *tile_gt, uint32_t *tile_eq, uint32_t nt, uint32_t *sh) {
@@ -418,90 +555,20 @@ __device__ __noinline__ void scan_tiles1(uint32_t *tile_gt, uint32_t *tile_eq, u
     }
 }
 
-// PICK: T's band bin from the fine histogram and the keys >= H, or a miss
-__device__ __noinline__ void pick_band(const T1Args &A, T1Lds &L) {
-    const uint32_t tid = threadIdx.x, nt = A.nt;
-    const uint32_t r = A.k - 1u;  // T's descending rank
-    uint32_t hi = 0;
-    for (uint32_t t = tid; t < nt; t += STG_WG) hi += ld_sc1(&A.sup_hi[t]);
-    constexpr uint32_t PER = NB_BAND / STG_WG;
-    uint32_t c[PER], s = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        c[j] = ld_sc1(&A.fine[NB_BAND - 1u - (PER * tid + j)]);
-        s += c[j];
-    }
-    uint32_t th, tband;
-    (void)blk_excl_scan<STG_WAVES>(hi, L.sh, &th);
-    if (tid == 0) L.v[2] = 0xffffffffu;
-    uint32_t above = blk_excl_scan<STG_WAVES>(s, L.sh, &tband);
-    const bool hit = th <= r && r < th + tband;
-    const uint32_t rr = r - th;
-    if (hit) {
-#pragma unroll
-        for (uint32_t j = 0; j < PER; ++j) {
-            if (above <= rr && rr < above + c[j]) { L.v[2] = NB_BAND - 1u - (PER * tid + j); L.v[3] = rr - above; }
-            above += c[j];
+// the count, then the failure word again: a select_broken (fail bit, then
+// POISON_COUNT) that came before the second read is seen there and poisoned
+// here; one that came after it stores its poison after ours
+__device__ __forceinline__ void write_count(const T1Args &A) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (!(ld_sc1(A.fail) & FAIL_SELECT)) {
+            st_sc1(A.count_out, A.cap);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (ld_sc1(A.fail) & FAIL_SELECT) st_sc1(A.count_out, POISON_COUNT);
         }
-    }
-    // the histogram back to zero for the next call (16-byte sc1 stores)
-    for (uint32_t i = tid; i < NB_BAND / 4u; i += STG_WG) st_sc1_zero16(A.fine, NB_BAND * 4u, 16u * i);
-    __syncthreads();
-    if (tid == 0) {
-        const bool ok = hit && L.v[2] != 0xffffffffu;
-        st_sc1(&A.ctl->miss, ok ? 0u : 1u);
-        st_sc1(&A.ctl->pick_bin, ok ? L.v[2] : 0u);
-        st_sc1(&A.ctl->pick_rin, ok ? L.v[3] : 0u);
-        if (!ok) A.state->inc = fminf(2.0f * A.state->inc, 0.5f);
     }
 }
 
-// EXACT: T from the bin's list, its keys into the per-tile counts, the
-// prefixes, the next hint -- or a miss (a crowded bin)
-__device__ __noinline__ void exact_band(const T1Args &A, T1Lds &L) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t nb = ld_sc1(&A.ctl->nbin_list), rin = ld_sc1(&A.ctl->pick_rin);
-    if (nb > BINL || rin >= nb) {
-        if (tid == 0) {
-            st_sc1(&A.ctl->miss, 1u);
-            A.state->inc = fminf(2.0f * A.state->inc, 0.5f);
-        }
-        return;
-    }
-    for (uint32_t i = tid; i < nb; i += STG_WG) {
-        const uint64_t w = ld_sc1(reinterpret_cast<const uint64_t *>(A.ctl->binl) + i);
-        L.u.bl[i] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < nb; i += STG_WG) {  // T: the key of descending rank rin in the bin
-        const uint32_t key = L.u.bl[i].y;
-        uint32_t gt = 0, eq = 0;
-        for (uint32_t x = 0; x < nb; ++x) { gt += L.u.bl[x].y > key; eq += L.u.bl[x].y == key; }
-        if (gt <= rin && rin < gt + eq) L.v[4] = key;
-    }
-    __syncthreads();
-    const uint32_t T = L.v[4];
-    for (uint32_t i = tid; i < nb; i += STG_WG) {
-        const uint2 x = L.u.bl[i];
-        if (x.y > T) g_add(&A.tile_gt[x.x / TV_TILE], 1u);
-        else if (x.y == T) g_add(&A.tile_eq[x.x / TV_TILE], 1u);
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    scan_tiles1(A.tile_gt, A.tile_eq, A.nt, L.sh);
-    if (tid == 0) {
-        const float Tp = A.state->t, d = A.state->inc, Tf = u2f(T);
-        A.state->t = Tf;  // the next call's hint; the band narrows while T keeps landing near its middle
-        A.state->inc = fabsf(Tf - Tp) < 0.25f * d * Tp ? fmaxf(0.75f * d, 1.0f / 512.0f) : d;
-        st_sc1(&A.ctl->res_T, T);
-        st_sc1(&A.ctl->miss, 0u);
-        atomicAdd(&A.dbg[38], 1u);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// the launch
-// ---------------------------------------------------------------------------
 // 2 workgroups per CU at least (<= 128 VGPRs); each phase body is its own
 // function within that budget
 template <bool VEC>
@@ -515,16 +582,52 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     __syncthreads();
     TopkCtl *const C = A.ctl;
     if (blockIdx.x == 0) TK1_STAMP(40);
-    if (blockIdx.x == 0) {  // the next call's control block (this call never touches it)
-        constexpr uint32_t W4 = (uint32_t)(offsetof(TopkCtl, binl) / 16);
-        for (uint32_t i = tid; i < W4; i += STG_WG)
-            st_sc1_zero16(reinterpret_cast<uint32_t *>(A.ctl_next), (uint32_t)offsetof(TopkCtl, binl), 16u * i);
+    {   // the next call's control block and band histogram, in shares (this call never touches them)
+        constexpr uint32_t CW = (uint32_t)(sizeof(TopkCtl) / 16), FW = TK2_FINE / 4u;
+        for (uint32_t i = blockIdx.x * STG_WG + tid; i < CW + FW; i += gridDim.x * STG_WG) {
+            if (i < CW) st_sc1_zero16(reinterpret_cast<uint32_t *>(A.ctl_next), (uint32_t)sizeof(TopkCtl), 16u * i);
+            else st_sc1_zero16(A.fine_next, TK2_FINE * 4u, 16u * (i - CW));
+        }
     }
-    const Band B = band_of(A.state);
+    if (blockIdx.x == 0) TK1_STAMP(41);  // workgroup 0: zeroing done
     const uint32_t home = blockIdx.x % TK1_SH;
     auto poison = [&]() {
-        if (tid == 0) { g_or(A.fail, FAIL_SPIN_TIMEOUT); st_sc1(A.count_out, POISON_COUNT); }
+        if (tid == 0) {
+            g_or(A.fail, FAIL_SPIN_TIMEOUT);
+            __hip_atomic_fetch_max(gp(A.count_out), POISON_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     };
+    // the band's way
+    Pick P;
+    const bool hit = !A.force_miss && pick_exact(A, L, P);
+    if (blockIdx.x == 0) TK1_STAMP(42);  // workgroup 0: pick done
+    TK1_STAMP_MAX(43);                   // every workgroup's pick done
+    if (hit) {
+        if (blockIdx.x == 0 && tid == 0) {  // the next call's hint; the band narrows while T keeps landing near T_prev
+            const float Tp = A.state->t, d = A.state->inc, Tf = u2f(P.T);
+            A.state->t = Tf;
+            A.state->inc = fabsf(Tf - Tp) < 0.25f * d * Tp ? fmaxf(0.75f * d, D_MIN) : fminf(d, D_MAX);
+            atomicAdd(&A.dbg[38], 1u);
+        }
+        const uint64_t need_eq = (uint64_t)A.k - P.gt;
+        const uint32_t NU = (A.nt + A.ut - 1u) / A.ut;
+        if (blockIdx.x >= NU) return;  // NU workgroups take the units (NU tickets on the counter word)
+        for (;;) {
+            if (tid == 0) L.v[9] = ld_sc1(&C->utk[0]) >= NU ? NU : g_add(&C->utk[0], 1u);
+            __syncthreads();
+            const uint32_t u = L.v[9];
+            __syncthreads();
+            if (u >= NU) break;
+            TK1_STAMP_MAX(48);  // the last unit taken
+            if (!emit_unit(A, L, u, P.T, need_eq)) { poison(); return; }
+            TK1_STAMP_MAX(44);  // the last unit done
+        }
+        TK1_STAMP_MAX(45);      // the last workgroup out
+        return;
+    }
+    if (blockIdx.x == 0 && tid == 0 && ld_sc1(&C->band_ok)) {  // a hinted call missed: widen the band
+        A.state->inc = fminf(2.0f * A.state->inc, D_MAX);
+    }
     // wait for the single-unit phase p's flag (one lane polls, sparsely)
     auto wait_flag = [&](uint32_t p) -> bool {
         if (tid == 0) {
@@ -543,13 +646,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     };
     // the single-unit phase p + 1 after multi-unit phase p
     auto run_single = [&](uint32_t p) {
-        if (p == P_STREAM) TK1_STAMP(41);
-        if (p == P_COUNT) TK1_STAMP(43);
-        if (p == P_STREAM) {
-            pick_band(A, L);
-        } else if (p == P_COUNT) {
-            exact_band(A, L);
-        } else if (p == M_H1) {
+        if (p == M_H1) {
             pick_level<20, 11, STG_WG, RS_SHARDS>(A.rs, A.zeros, A.k - 1u);
         } else if (p == M_H2) {
             pick_level<9, 11, STG_WG, RS_SHARDS>(A.rs, A.zeros, 0);
@@ -562,7 +659,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
                 st_sc1(&C->res_T, T);
                 atomicAdd(&A.dbg[39], 1u);
                 A.state->t = u2f(T);
-                if (!A.state->init) A.state->inc = 1.0f / 64.0f;
+                if (!A.state->init) A.state->inc = D_SEED;
                 A.state->init = 1;
             }
         } else if (p == M_CNT) {
@@ -570,33 +667,26 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         }
         vm_drain();
         __syncthreads();
-        if (p == P_STREAM) TK1_STAMP(42);
-        if (p == P_COUNT) TK1_STAMP(44);
         if (tid == 0) st_sc1(&C->flag[p + 1], A.tag);
     };
     // one multi-unit phase: take units until every shard is empty; the
     // workgroup completing the phase also runs the single-unit phase after it
-    uint32_t blo = 0, bhi = 0;
-    auto run_multi = [&](uint32_t p, uint32_t T, uint64_t need_eq, bool from_sup) {
+    auto run_multi = [&](uint32_t p, uint32_t T, uint64_t need_eq) {
         const uint32_t U = A.nt, nsh = min(U, TK1_SH);
         for (uint32_t si = 0; si < TK1_SH; ++si) {
             const uint32_t s = (home + si) % TK1_SH, su = shard_units(U, s);
             for (;;) {
-                if (tid == 0) {  // a plain look first: an empty shard costs no atomic
+                if (tid == 0)  // a plain look first: an empty shard costs no atomic
                     L.v[9] = ld_sc1(&C->tk[p][s][0]) >= su ? su : g_add(&C->tk[p][s][0], 1u);
-                    L.v[1] = 0;
-                }
                 __syncthreads();
                 const uint32_t c = L.v[9];
                 if (c >= su) { __syncthreads(); break; }
                 const uint32_t tile = s + TK1_SH * c;
-                if (p == P_STREAM) unit_stream<VEC>(A, L, tile, B);
-                else if (p == P_COUNT) unit_countband<VEC>(A, L, tile, blo, bhi);
-                else if (p == M_H1) unit_hist<VEC, 20, 11>(A, L, tile);
+                if (p == M_H1) unit_hist<VEC, 20, 11>(A, L, tile);
                 else if (p == M_H2) unit_hist<VEC, 9, 11>(A, L, tile);
                 else if (p == M_H3) unit_hist<VEC, 0, 9>(A, L, tile);
                 else if (p == M_CNT) unit_count<VEC>(A, L, tile);
-                else unit_emit<VEC>(A, L, tile, T, need_eq, from_sup);
+                else unit_emit<VEC>(A, L, tile, T, need_eq);
                 vm_drain();
                 __syncthreads();
                 if (tid == 0) {
@@ -606,44 +696,17 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
                 }
                 __syncthreads();
                 if (L.v[10]) {
-                    if (p == P_EMIT) {  // the count, then the failure word again (see topk.hip)
-                        TK1_STAMP(45);
-                        if (tid == 0) {
-                            __builtin_amdgcn_s_waitcnt(0);
-                            if (!(ld_sc1(A.fail) & FAIL_SELECT)) {
-                                st_sc1(A.count_out, A.cap);
-                                __builtin_amdgcn_s_waitcnt(0);
-                                if (ld_sc1(A.fail) & FAIL_SELECT) st_sc1(A.count_out, POISON_COUNT);
-                            }
-                        }
-                    } else {
-                        run_single(p);
-                    }
+                    if (p == P_EMIT) write_count(A);
+                    else run_single(p);
                 }
                 __syncthreads();
             }
         }
     };
-    bool miss = !A.hinted;
-    if (!miss) {
-        run_multi(P_STREAM, 0, 0, false);
-        if (!wait_flag(P_PICK)) { poison(); return; }
-        miss = ld_sc1(&C->miss) != 0;
-        if (!miss) {
-            const uint32_t b = ld_sc1(&C->pick_bin);
-            blo = B.F + (b << B.sh);
-            bhi = min(B.H, blo + (1u << B.sh));
-            run_multi(P_COUNT, 0, 0, false);
-            if (!wait_flag(P_EXACT)) { poison(); return; }
-            miss = ld_sc1(&C->miss) != 0;
-        }
-    }
-    if (miss) {
-        const uint32_t seq[4] = {M_H1, M_H2, M_H3, M_CNT};
-        for (uint32_t i = 0; i < 4; ++i) {
-            run_multi(seq[i], 0, 0, false);
-            if (!wait_flag(seq[i] + 1u)) { poison(); return; }
-        }
+    const uint32_t seq[4] = {M_H1, M_H2, M_H3, M_CNT};
+    for (uint32_t i = 0; i < 4; ++i) {
+        run_multi(seq[i], 0, 0);
+        if (!wait_flag(seq[i] + 1u)) { poison(); return; }
     }
     const uint32_t T = ld_sc1(&C->res_T);
     const uint64_t tgt = ld_sc1(&A.tile_gt[2 * A.nt]), teq = ld_sc1(&A.tile_eq[2 * A.nt]);
@@ -656,8 +719,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
             A.val[s] = 0.f;
         }
     }
-    if (blockIdx.x == 0) TK1_STAMP(46);  // workgroup 0 reaches the emission
-    run_multi(P_EMIT, T, need_eq, !miss);
+    run_multi(P_EMIT, T, need_eq);
 }
 
 }  // namespace
@@ -674,6 +736,24 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     }
     const uint32_t nt = (uint32_t)((m + TV_TILE - 1) / TV_TILE);
     if (nt > TOPK_LIST_TILES) return hipErrorInvalidValue;
+    if (!hinted) {  // a key's first call: the select's launches, then the hint
+        hipError_t e = launch_topk(a, ws, s);
+        if (e != hipSuccess) return e;
+        tk2_seed<<<1, 1, 0, s>>>(state, ws.rsel, ws.misc);
+        return hipGetLastError();
+    }
+    TopkCtl *const ctl = ws.tkctl + (tag & 1u);
+    uint32_t *const fine = ws.tkfine + (size_t)(tag & 1u) * TK2_FINE;
+    // superset regions: the bucket's share of TOPK_SUP_CAP entries per tile, in TK1_SH regions
+    const uint32_t shard_cap = (uint32_t)((size_t)nt * TOPK_SUP_CAP / TK1_SH);
+    uint32_t *const sup_n = ws.tile_cnt + 2 * (size_t)nt + 1, *const sup_off = ws.tile_aux + 2 * (size_t)nt + 1;
+    uint2 *const sup = reinterpret_cast<uint2 *>(ws.sums);
+    const bool vec = (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0;
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    T2Stream S{a.src, m, last_mask, nt, state, ctl, fine, sup, shard_cap, sup_n, sup_off, a.count_out, a.cap};
+    if (vec) tk2_stream<true><<<nt, STG_WG, 0, s>>>(S);
+    else tk2_stream<false><<<nt, STG_WG, 0, s>>>(S);
+    if (a.ev) (void)hipEventRecord(a.ev[1], s);
     T1Args A{};
     A.a = a.src;
     A.m = m;
@@ -689,24 +769,29 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     A.count_out = a.count_out;
     A.fail = ws.fail;
     A.state = state;
-    A.hinted = hinted;
-    A.ctl = ws.tkctl + (tag & 1u);
+    A.ctl = ctl;
     A.ctl_next = ws.tkctl + ((tag + 1u) & 1u);
     A.tag = tag;
     A.rs = ws.rsel;
-    A.sup = reinterpret_cast<uint2 *>(ws.sums);
+    A.sup = sup;
+    A.shard_cap = shard_cap;
+    A.sup_n = sup_n;
+    A.sup_off = sup_off;
     A.tile_gt = ws.tile_cnt;
     A.tile_eq = ws.tile_aux;
-    A.sup_n = ws.tile_cnt + 2 * (size_t)nt + 1;
-    A.sup_hi = ws.tile_aux + 2 * (size_t)nt + 1;
-    A.fine = ws.tkfine;
+    A.fine = fine;
+    // a unit's superset (~ k / nt entries per tile) in about one round of ER per thread
+    A.ut = (uint32_t)std::max<uint64_t>((nt + TK2_UNITS - 1) / TK2_UNITS,
+                                        std::min<uint64_t>(TK2_UT, (uint64_t)ER * STG_WG * nt / std::max<uint64_t>(A.k, 1)));
+    A.ut = std::max(1u, std::min(A.ut, TK2_UT));
+    A.fine_next = ws.tkfine + (size_t)((tag + 1u) & 1u) * TK2_FINE;
     A.dbg = ws.misc;
     const uint32_t G = std::min<uint32_t>(nt, (uint32_t)a.num_cu * 2u);
-    if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    const bool vec = (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0;
+    static const int dbg_mode = getenv("STG_TK1_DEBUG") ? atoi(getenv("STG_TK1_DEBUG")) : 0;
+    A.force_miss = dbg_mode == 2;
     if (vec) tk_one<true><<<G, STG_WG, 0, s>>>(A);
     else tk_one<false><<<G, STG_WG, 0, s>>>(A);
-    if (a.ev) { (void)hipEventRecord(a.ev[1], s); (void)hipEventRecord(a.ev[2], s); }
+    if (a.ev) (void)hipEventRecord(a.ev[2], s);
     return hipGetLastError();
 }
 

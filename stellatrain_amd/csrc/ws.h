@@ -103,27 +103,36 @@ struct CrewCtl {
     uint32_t beta, nL, status, P, tail_rank, op, pad[2];
 };
 
-// top-k in one launch (topk1.hip): per-call control block, two copies by call
-// tag parity (each call zeroes the next call's), and the band histogram
-constexpr uint32_t TK1_NPH = 13;    // phases
-constexpr uint32_t TK1_SH = 8;      // ticket / completion shards (tile % 8)
+// top-k steered by the key's last k-th magnitude (topk1.hip): per-call control
+// block, two copies by call tag parity (each call zeroes the next call's), and
+// the band histogram (one bin per ulp, two copies by parity)
+constexpr uint32_t TK1_NPH = 9;     // phases of the select's way
+constexpr uint32_t TK1_SH = 8;      // ticket / completion shards (tile % 8); superset regions
 constexpr uint32_t TK1_LINE = 32;   // words per 128-byte line: every shard counter on a line of its own
-constexpr uint32_t TK1_FINE = 8192; // band histogram bins
-constexpr uint32_t TK1_BINL = 2048; // entries of T's band bin listed (more: the select's way)
+constexpr uint32_t TK2_FINE = 1u << 18;               // band bins: one per ulp
+constexpr uint32_t TK2_CSH = 8;                       // coarse bins: 256 ulps
+constexpr uint32_t TK2_COARSE = TK2_FINE >> TK2_CSH;  // 1024
+constexpr uint32_t TK2_HI = 16;                       // shards of the count of keys above the band
+constexpr uint32_t TK2_UT = 16;                       // tiles per emission unit
+constexpr uint32_t TK2_UNITS = TOPK_LIST_TILES / TK2_UT;
 struct alignas(128) TopkCtl {
     uint32_t tk[TK1_NPH][TK1_SH][TK1_LINE];    // tickets per phase and shard
     uint32_t done[TK1_NPH][TK1_SH][TK1_LINE];  // units done per phase and shard
     uint32_t sdone[TK1_NPH][TK1_LINE];         // shards done per phase
     uint32_t flag[TK1_NPH];                    // = the call tag once single-unit phase p is done
-    uint32_t miss, res_T, pick_bin, pick_rin, nbin_list;
+    uint32_t band_F, band_H, band_ok, ovf, res_T;  // the stream launch's band [F, H); a superset region overflowed
     uint32_t pad[TK1_LINE - TK1_NPH - 5];
-    uint2 binl[TK1_BINL];                      // {element, key} of T's band bin
+    uint32_t utk[TK1_LINE];                    // emission units taken
+    uint32_t hi[TK2_HI][TK1_LINE];             // keys >= H, by tile % TK2_HI
+    uint32_t shn[TK1_SH][TK1_LINE];            // superset entries placed in region tile % 8
+    uint32_t coarse[TK2_COARSE];               // band keys per 256 ulps
+    uint64_t udesc[TK2_UNITS];                 // emission unit u: bit 63 | > T count << 32 | == T count
 };
 
 struct DevWS {
     FillCtl *ctl;
     TopkCtl *tkctl;      // [2]
-    uint32_t *tkfine;    // TK1_FINE words, zero between calls
+    uint32_t *tkfine;    // [2][TK2_FINE] band histograms by call parity, zero between calls
     CrewCtl *crew;       // MAX_BATCH slots
     ChunkDesc *desc;     // thresholdv16 chunk descriptors (grown per launch, zeroed)
     CallParams *cp;
@@ -268,8 +277,10 @@ struct TopkLaunch {
     hipEvent_t *ev;
 };
 hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s);
-// top-k in one launch steered by the key's last k-th magnitude (topk1.hip);
-// buckets of at most TOPK_LIST_TILES tiles
+// top-k steered by the key's last k-th magnitude (topk1.hip), buckets of at
+// most TOPK_LIST_TILES tiles: a key's first call (!hinted) runs launch_topk and
+// seeds the hint; later calls stream once and emit (the select's way inside
+// the emission launch when the band misses)
 hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, bool hinted, uint32_t tag,
                         hipStream_t s);
 

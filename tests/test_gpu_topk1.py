@@ -1,9 +1,9 @@
-"""Top-k in one launch, steered by the key's last k-th magnitude (topk1.hip).
+"""Top-k in one pass over the bucket, steered by the key's last k-th magnitude (topk1.hip).
 
-A key's first call takes the select's way inside the launch; later calls stream
+A key's first call takes the select's launches (topk.hip); later calls stream
 the bucket once against a band around the last k-th magnitude and resolve T
 inside it; a band that misses (the magnitudes jump) falls back to the select
-inside the same launch and widens.  Every call is checked against the oracle:
+inside the emission launch and widens.  Every call is checked against the oracle:
 the whole stream for the corrected mode, the signed value multiset (freedom
 only at the k-th magnitude) for the shipped mode.  Debug words 38 / 39 count
 calls resolved in the band / by the select.

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Phase times of the one-launch top-k (topk1.hip) from a stamp build
-(-DSTG_TK1_STAMPS=1, STG_CODEC_LIB): us after the kernel start of STREAM
-complete, PICK done, COUNT complete, EXACT done, workgroup 0 at EMIT, EMIT
-complete; 8 steady calls per mode on the C2 bucket (64 MiB, k = 1 %)."""
+"""Phase times of the emission launch of the hinted top-k (topk1.hip tk_one)
+from a stamp build (-DSTG_TK1_STAMPS=1, STG_CODEC_LIB): us after workgroup 0
+starts of its zeroing done, its pick done, every workgroup's pick done, the
+last emission unit done, the last workgroup out; plus the two launches'
+event times; 10 calls per mode on the C2 bucket (64 MiB, k = 1 %)."""
 import ctypes as C
 import json
 import os
@@ -29,15 +30,19 @@ def main():
     val = torch.zeros(k, dtype=torch.float32, device=dev)
     for exact in (True, False):
         comp = TopkCompressor(exact=exact)
+        comp.set_timing(True)
         for c in range(10):
             comp.compress("c2", bufs[c % 4], k, idx, val)
+            (k0, k1, kall), launches = comp.get_timing()
             w = (C.c_uint32 * 64)()
             check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
             w = list(w)
             t0 = w[40]
             rel = {name: round(((w[i] - t0) & 0xffffffff) / 100.0, 2) for name, i in
-                   (("stream", 41), ("pick", 42), ("count", 43), ("exact", 44), ("wg0_emit", 46), ("emit", 45))}
-            print(json.dumps({"exact": exact, "call": c, "hits": w[38], "selects": w[39], "us": rel}), flush=True)
+                   (("wg0_zeroed", 41), ("wg0_pick", 42), ("all_pick", 43), ("last_taken", 48), ("last_counted", 46),
+                    ("last_lookback", 47), ("last_unit", 44), ("last_out", 45))}
+            print(json.dumps({"exact": exact, "call": c, "hits": w[38], "selects": w[39], "us": rel,
+                              "event_us": {"stream": round(k0 * 1e3, 2), "emit": round(k1 * 1e3, 2)}}), flush=True)
 
 
 if __name__ == "__main__":
