@@ -1224,6 +1224,7 @@ tv16_fill(Tv16FillArgs A) {
             I.lvl1 = NONE;
             I.r1 = 0;
             I.gcap = 2u * (d.nb + 64u);
+            I.positions = true;
             const LeadOut O = leader(Wl, I);
             if (O.ok) {
                 const uint32_t *const opos = O.ordpos;

@@ -119,11 +119,14 @@ struct LeadIn {
     uint32_t gcap;
     uint32_t *dbg;                 // stamp builds: the leader's step times, words 24..28
     uint32_t lvl1, r1;             // lvl1 != NONE: the key at rank sel has top 13 bits lvl1, rank r1 among them
+    bool positions;                // also resolve the pops' element positions (ordpos); the crew's
+                                   // emission units resolve them from `order` themselves
 };
 struct LeadOut {
     bool ok;
     uint32_t P, tail_rank;
-    const uint32_t *ordpos;  // element position of each pop
+    const uint32_t *ordpos;  // element position of each pop (I.positions)
+    const uint32_t *order;   // list entry of each pop (| 2^31 when tied)
     uint32_t why;            // failure: 1 NaN, 2 scratch, 3 crowded bin / rank not found, 4 short list, 5 roots, 6 height, 7 late, 8 run
 };
 
@@ -223,7 +226,10 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
     const uint32_t tid = threadIdx.x;
     // Loads go through this XCD's L2 (cached: the list and the scratch are
     // read many times); the acquire drops lines other XCDs have since written.
-    // Stores stay sc1 (write-through: the L2 line and memory both updated).
+    // The scratch only this workgroup reads is stored plain (its L2): on this
+    // chip vmcnt counts stores with loads, in order, so a load issued after an
+    // sc1 store (written through to HBM) waits for that store.  What other
+    // workgroups read (the pops' order, their positions) is stored sc1.
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const uint32_t n = uni(I.n), tail = uni(I.tail), tbits = uni(I.tail_bits), NN = uni(I.N);
     const uint32_t m = n + tail;
@@ -403,8 +409,8 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                 tie |= x != j && (uint32_t)(kx >> 32) == (uint32_t)(key >> 32);
             }
             tie_any |= tie ? 1u : 0u;
-            st_sc1(&go[rk], W.u.s.ti[j] | (tie ? 0x80000000u : 0u));
-            st_sc1(&gs[rk], key);
+            go[rk] = W.u.s.ti[j] | (tie ? 0x80000000u : 0u);
+            gs[rk] = key;
         }
         __syncthreads();
         if (s0 == 0) LEAD_SUB(7);
@@ -534,12 +540,12 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
             // positions: starts, then replays
             each_b<u4v>(nq, [&](uint32_t q) { return ld4(rc, q); }, [&](uint32_t q, u4v x) {
                 const uint32_t i = 4u * q;
-                st_sc1(&gp[i], x.x);
-                if (i + 1u < n) st_sc1(&gp[i + 1u], x.y);
-                if (i + 2u < n) st_sc1(&gp[i + 2u], x.z);
-                if (i + 3u < n) st_sc1(&gp[i + 3u], x.w);
+                gp[i] = x.x;
+                if (i + 1u < n) gp[i + 1u] = x.y;
+                if (i + 2u < n) gp[i + 2u] = x.z;
+                if (i + 3u < n) gp[i + 3u] = x.w;
             });
-            if (tail && tid == 0) st_sc1(&gp[n], NN - 1u);
+            if (tail && tid == 0) gp[n] = NN - 1u;
             vm_drain();
             __syncthreads();
             uint32_t late_bad = 0;
@@ -610,7 +616,7 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                     const uint2 x = sim[l];
                     if (x.y == NONE) continue;
                     const uint32_t t = depth_of(l + 1u), p = (qa << t) - 1u + (l - ((1u << t) - 1u));
-                    st_sc1(&gp[x.y], p);
+                    gp[x.y] = p;
                     if (p >= late_lo) late_bad = 1;  // an R_smin line stays where pop_heap re-inserts
                 }
                 vm_drain();
@@ -647,7 +653,7 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                     if (g1 - g0 >= WRUN) { big = 1; continue; }
                     uint32_t rk = g0;
                     for (uint32_t x = g0; x < g1; ++x) rk += rfk[x] < kj;
-                    st_sc1(&go[s0 + rk], o);
+                    go[s0 + rk] = o;
                 }
                 vm_drain();
                 if (__syncthreads_or((int)big)) { O.why = 8; return O; }
@@ -669,14 +675,29 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
     uint32_t P = P0;
     if (tr < P0) P = (uni(I.rem) + (16u - uni(I.tl)) + 15u) / 16u;
     if (P > nr) { O.why = 4; return O; }
-    each_b2<uint32_t, uint32_t>(P, [&](uint32_t i) { return ldc(&go[i]) & LNONE; }, [&](uint32_t, uint32_t e) { return ps(e); },
-                                [&](uint32_t i, uint32_t, uint32_t p) { st_sc1(&op[i], p); });
+    // go was stored plain: the order for other workgroups (the crew's
+    // emission units) is written through here, sc1 and coalesced
+    for (uint32_t i0 = 0; i0 < P; i0 += WB * FILL_WG) {
+        uint32_t x[WB];
+#pragma unroll
+        for (uint32_t b = 0; b < WB; ++b) x[b] = ldc(&go[min(i0 + b * FILL_WG + tid, P - 1u)]);
+#pragma unroll
+        for (uint32_t b = 0; b < WB; ++b)
+            if (i0 + b * FILL_WG + tid < P) st_sc1(&go[i0 + b * FILL_WG + tid], x[b]);
+    }
+    if (I.positions) {
+        each_b2<uint32_t, uint32_t>(P, [&](uint32_t i) { return ldc(&go[i]) & LNONE; }, [&](uint32_t, uint32_t e) { return ps(e); },
+                                    [&](uint32_t i, uint32_t, uint32_t p) { st_sc1(&op[i], p); });
+        vm_drain();
+        __syncthreads();
+    }
     vm_drain();
     __syncthreads();
     LEAD_STAMP(4);
     O.P = P;
     O.tail_rank = tr;
     O.ordpos = op;
+    O.order = go;
     O.ok = true;
     return O;
 }
@@ -953,11 +974,13 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
             I.dbg = A.dbg;
             I.lvl1 = beta;
             I.r1 = ld_sc1(&ctl->pad[0]);
+            I.positions = false;
             if (STG_CREW_STAMPS && tid == 0) A.dbg[29] = (uint32_t)__builtin_amdgcn_s_memrealtime();
             LeadOut O;
             O.ok = false;
             O.tail_rank = NONE;
             O.ordpos = cm.keys;
+            O.order = cm.keys;
             if (STG_CREW_STAMPS >= 2 && !ovf) {  // diagnostics: a first run warms the caches
                 (void)leader(W, I);
                 __syncthreads();
@@ -970,7 +993,7 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
                 if (!ok) atomicAdd(&A.dbg[55], 1u);
                 st_sc1(&ctl->P, ok ? O.P : 0u);
                 st_sc1(&ctl->tail_rank, O.tail_rank);
-                st_sc1(&ctl->op, ok ? (uint32_t)(O.ordpos - cm.keys) : 0u);
+                st_sc1(&ctl->op, ok ? (uint32_t)(O.order - cm.keys) : 0u);
             }
             if (!ok) {  // exact, slow; its LDS view covers this workgroup's plan, so it takes no more units
                 const CrewBk Bl = B;
@@ -981,12 +1004,23 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
                 if (tid == 0) g_add(&done[p], 1u);
                 return;
             }
-        } else {  // E: emission share `rel`
-            const uint32_t P = ld_sc1(&ctl->P), tr = ld_sc1(&ctl->tail_rank);
-            const uint32_t *const op = crew_map(B).keys + ld_sc1(&ctl->op);
+        } else {  // E: emission share `rel`: the pops' list entries -> element positions (LDS), then the lines
+            const uint32_t P = ld_sc1(&ctl->P), tr = ld_sc1(&ctl->tail_rank), nL = ld_sc1(&ctl->nL);
+            const CrewMap cm = crew_map(B);
+            const uint32_t *const go = cm.keys + ld_sc1(&ctl->op);
+            const uint32_t *const lp = cm.lp;
+            const uint32_t tpos = uni(B.d.nb) * 16u, nl1 = nL ? nL - 1u : 0u;
             const uint32_t per = (P + CW_NE - 1u) / CW_NE;
-            if (P && rel * per < P)
-                emit_order(B.d, B.cnt, B.rem, P, tr, [&](uint32_t i) { return ld_sc1(&op[i]); }, rel * per, (rel + 1u) * per);
+            uint32_t *const posl = W.u.s.hist;  // WBINS words
+            for (uint32_t i0 = rel * per, i1 = min(P, (rel + 1u) * per); i0 < i1; i0 += WBINS) {
+                const uint32_t ie = min(i1, i0 + WBINS);
+                each_b2<uint32_t, uint32_t>(ie - i0, [&](uint32_t j) { return ld_sc1(&go[i0 + j]) & LNONE; },
+                                            [&](uint32_t, uint32_t e) { const uint32_t x = ld_sc1(&lp[min(e, nl1)]); return e < nL ? x : tpos; },
+                                            [&](uint32_t j, uint32_t, uint32_t p) { posl[j] = p; });
+                __syncthreads();
+                emit_order(B.d, B.cnt, B.rem, P, tr, [&](uint32_t i) { return posl[i - i0]; }, i0, ie);
+                __syncthreads();
+            }
         }
         vm_drain();
         __syncthreads();
