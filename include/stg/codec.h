@@ -111,6 +111,22 @@ int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
 int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, float *const *d_residuals,
                                     size_t nbuckets, void *stream);
 
+/* One MERGE task with the intra-node gather ahead of it (ModuleCpuGather::run
+ * then ModuleCompress::run on local rank r's slice, engine/modules/
+ * cpu_gather.cpp:59-87 and compress.cpp:139-186).  bucket->d_src is grad[0]'s
+ * slice: it receives d_residual (may be null) + d_grads[1] + ... +
+ * d_grads[num_gpus - 1] (slice pointers, [0] ignored, peers' over xGMI) in
+ * stg_gather_add_device's order, is compressed, and when d_residual is not
+ * null its error feedback runs as in stg_merge_compress_batch_device.  The
+ * same results as stg_gather_add_device, then stg_merge_compress_batch_device
+ * (d_residual) or stg_codec_compress_device (no residual), on one bucket.
+ * thresholdv16 sums the sources inside its one-bucket streaming pass (each
+ * source read once, grad[0] stored once, the line sums taken from the sum):
+ * one pass instead of the gather's and the codec's.  A key's first call, and
+ * the other codecs, run the gather-add pass first.  Async on `stream`. */
+int stg_merge_gather_compress_device(stg_codec_t h, const stg_bucket_t *bucket, float *d_residual,
+                                     const float *const *d_grads, int num_gpus, void *stream);
+
 /* Per-key AIMD state (thresholdv16.cpp:243-259, thresholdv.cpp:72-80), read
  * back for parity tests; synchronises `stream`.  Returns STG_ERR_INVALID when
  * the key has never been compressed.  For threshold-v pass the src pointer

@@ -142,6 +142,36 @@ class Compressor:
         check(lib().stg_merge_compress_batch_device(self._h, arr, rp, len(items), C.c_void_p(sp)))
         return counts
 
+    def merge_gather_compress_async(self, name: str, grads, k: int, dst_idx, dst_val, residual=None,
+                                    idx_offset: int = 0, count=None, stream=None):
+        """One MERGE task with the intra-node gather ahead of it
+        (``stg_merge_gather_compress_device``; cpu_gather.cpp:59-87, then
+        compress.cpp:139-186): ``grads[0] += residual + grads[1] + ... +
+        grads[N-1]`` (this rank's slices, left to right), compress grads[0]
+        under ``name``, and with ``residual`` its error feedback.  thresholdv16
+        sums the sources inside its streaming pass.  Returns the int32 count
+        tensor (no host sync)."""
+        import torch
+        g0 = grads[0]
+        n = g0.numel()
+        for t in list(grads) + ([residual] if residual is not None else []) + [dst_idx, dst_val]:
+            if not (t.is_cuda and t.is_contiguous()):
+                raise ValueError("merge_gather_compress: contiguous device tensors")
+        for t in list(grads) + ([residual] if residual is not None else []):
+            if t.numel() != n or t.dtype != torch.float32:
+                raise ValueError("merge_gather_compress: float32 sources of one size")
+        if count is None:
+            count = torch.zeros(1, dtype=torch.int32, device=g0.device)
+        kb = name.encode()
+        b = StgBucket(kb, g0.data_ptr(), n, int(k), dst_idx.data_ptr(), dst_idx.numel(), dst_val.data_ptr(),
+                      dst_val.numel(), int(idx_offset), count.data_ptr())
+        ptrs = (C.c_void_p * len(grads))(*[t.data_ptr() for t in grads])
+        sp = stream if stream is not None else _stream_ptr(g0.device.index)
+        check(lib().stg_merge_gather_compress_device(
+            self._h, C.byref(b), C.c_void_p(residual.data_ptr()) if residual is not None else None, ptrs,
+            len(grads), C.c_void_p(sp)))
+        return count
+
     @staticmethod
     def bucket_array(rows):
         """Prebuilt ``stg_bucket_t`` array from raw tuples (key bytes, src_ptr,

@@ -463,7 +463,8 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
 // thresholdv16 over a sequence of buckets: runs of distinct keys (<= 16)
 // share one launch; the per-key state makes a repeated key wait for the
 // launch that updates it.
-int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s, float *const *resid = nullptr) {
+int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s, float *const *resid = nullptr,
+             const stg::GatherArgs *gather = nullptr) {
     HIP_TRY(hipSetDevice(h->device));
     Workspace *ws = nullptr;
     int rc = h->workspace(s, &ws);
@@ -496,6 +497,7 @@ int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s, fl
         t.state = st;
         t.first = fresh;
         t.resid = resid ? resid[i] : nullptr;
+        t.gather = i == 0 ? gather : nullptr;
         grp.push_back(t);
     }
     return launch_tv16_group(h, ws, grp, s);
@@ -788,6 +790,35 @@ int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
     for (size_t i = 0; i < nbuckets; ++i)
         if (buckets[i].n && (rc = ef_after(h, buckets[i], d_residuals[i], fused, s))) return rc;
     return STG_OK;
+}
+
+int stg_merge_gather_compress_device(stg_codec_t h, const stg_bucket_t *bucket, float *d_residual,
+                                     const float *const *d_grads, int num_gpus, void *stream) {
+    if (!h || !bucket) return fail(STG_ERR_INVALID, "null codec or bucket");
+    if (num_gpus < 1 || num_gpus > (int)stg::GATHER_MAX) return fail(STG_ERR_INVALID, "num_gpus must be in [1, 16]");
+    if (num_gpus > 1 && !d_grads) return fail(STG_ERR_INVALID, "null d_grads");
+    for (int i = 1; i < num_gpus; ++i)
+        if (bucket->n && !d_grads[i]) return fail(STG_ERR_INVALID, "null source");
+    const stg_bucket_t &b = *bucket;
+    int rc = validate(h, b.n, b.k, b.idx_cap, b.val_cap, b.d_count);
+    if (rc) return rc;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipSetDevice(h->device));
+    stg::GatherArgs g{};
+    g.dst = const_cast<float *>(b.d_src);
+    g.resid = d_residual;
+    g.nsrc = (uint32_t)num_gpus;
+    for (int i = 1; i < num_gpus; ++i) g.src[i] = d_grads[i];
+    if (h->method == M_TV16 && b.n) {
+        float *res[1] = {d_residual};
+        if ((rc = run_tv16(h, &b, 1, s, d_residual ? res : nullptr, &g))) return rc;
+        return d_residual ? ef_after(h, b, d_residual, true, s) : STG_OK;
+    }
+    // the other codecs: the gather-add pass, then the task as without it
+    HIP_TRY(stg::launch_gather_add(g, 0, b.n, h->num_cu, s));
+    if (d_residual) return stg_merge_compress_batch_device(h, &b, &d_residual, 1, stream);
+    return run_device(h, b.key, b.d_src, b.d_src, b.n, b.k, b.d_idx, b.idx_cap, b.d_val, b.val_cap, b.idx_offset,
+                      b.d_count, s);
 }
 
 int stg_codec_compress_host(stg_codec_t h, const char *key, const float *src, size_t n, uint32_t k,

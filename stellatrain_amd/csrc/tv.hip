@@ -22,6 +22,7 @@
 // order.  The last range folds the counts and maxima into the AIMD threshold
 // and the count.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ws.h"
 
@@ -77,6 +78,8 @@ struct TvArgs {
     uint64_t base;       // its value when this call starts (G per earlier call)
     uint32_t *fail;      // the workspace's sticky failure word
     uint32_t *dbg;       // diagnostics (STG_TV_STAMPS builds): phase stamps at words 40..49
+    uint32_t withhold;   // tests (STG_DEBUG_TV_WITHHOLD=1): range 0 never publishes its count, so every
+                         // later range's look-back runs out its bound: the failure path end to end
 };
 
 #ifndef STG_TV_STAMPS
@@ -204,7 +207,7 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
         uint32_t m = 0;
         for (uint32_t i = 0; i < TNW; ++i) m = max(m, s_max[i]);
         st_sc1(&a.rmax[r], ((uint64_t)a.tag << 32) | m);
-        st_sc1(&a.desc[r], ((uint64_t)a.tag << 32) | c);
+        if (!(a.withhold && r == 0)) st_sc1(&a.desc[r], ((uint64_t)a.tag << 32) | c);
     }
     // look-back: the counts of ranges 0 .. r-1 (taken earlier, so held by
     // running or finished workgroups), one per thread in one round trip;
@@ -346,6 +349,8 @@ hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s) {
     f.dbg = ws.misc;
     f.ticket = ws.tv_ticket;
     f.base = a.ticket_base;
+    static const bool withhold = getenv("STG_DEBUG_TV_WITHHOLD") && atoi(getenv("STG_DEBUG_TV_WITHHOLD")) == 1;
+    f.withhold = withhold && G > 1;
     if (a.grid_out) *a.grid_out = G;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     tv_pass<<<G, TWG, 0, s>>>(f);

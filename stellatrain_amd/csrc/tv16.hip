@@ -749,6 +749,29 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     BatchArgs A{};
     Tv16FillArgs F{};
     uint32_t K = 0;
+    static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
+    static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
+    // the one-bucket path: a scan with no waits between workgroups, finished
+    // by the fill launch (tv16lone.hip; STG_TV16_LFIN=0: the batched scan)
+    static const bool lfin_ok = !(getenv("STG_TV16_LFIN") && atoi(getenv("STG_TV16_LFIN")) == 0);
+    auto lone_chunks = [](size_t n) { return std::max<uint32_t>(1, (uint32_t)((n / 16 + LCHUNK - 1) / LCHUNK)); };
+    const bool lone_path = lone_ok && lfin_ok && a.nb == 1 && !dbg_stage && lone_chunks(a.b[0].n) <= a.lone_cap &&
+                           lone_chunks(a.b[0].n) <= LMAXC && ws.ldesc;
+    // a gather-add rides in the one-bucket scan (not on a key's first call,
+    // whose threshold is taken from the bucket before the scan); elsewhere it
+    // runs as its own pass first
+    bool fused_gather = false;
+    for (uint32_t i = 0; i < a.nb; ++i) {
+        const Tv16Bucket &b = a.b[i];
+        if (!b.gather || (!b.gather->resid && b.gather->nsrc <= 1)) continue;  // (no term to add)
+        if (b.gather->dst != b.src) return hipErrorInvalidValue;
+        if (lone_path && !b.first) {
+            fused_gather = true;
+        } else {
+            const hipError_t e = launch_gather_add(*b.gather, 0, b.n, a.num_cu, s);
+            if (e != hipSuccess) return e;
+        }
+    }
     for (uint32_t i = 0; i < a.nb; ++i) {
         const Tv16Bucket &b = a.b[i];
         if (b.first) {  // first threshold from sequential line sums (thresholdv16.cpp:36-54)
@@ -800,14 +823,9 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     // (all of them for one stream; launches from several streams split them);
     // no more than there are chunks.  Co-residency is not required.
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(a.max_wg, K), MAXG));
-    static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
-    static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
     const bool lone_scan = lone_ok && a.nb == 1;
-    // the one-bucket path: a scan with no waits between workgroups, finished
-    // by the fill launch (tv16lone.hip; STG_TV16_LFIN=0: the batched scan)
-    static const bool lfin_ok = !(getenv("STG_TV16_LFIN") && atoi(getenv("STG_TV16_LFIN")) == 0);
-    const uint32_t KL = std::max<uint32_t>(1, (A.bk[0].nb + LCHUNK - 1) / LCHUNK);  // one-bucket chunks
-    if (lone_scan && lfin_ok && !dbg_stage && KL <= a.lone_cap && KL <= LMAXC && ws.ldesc) {
+    const uint32_t KL = lone_chunks(a.b[0].n);  // one-bucket chunks
+    if (lone_path) {
         if (a.ev) (void)hipEventRecord(a.ev[0], s);
         LScanArgs L{};
         L.src = a.b[0].src;
@@ -823,6 +841,13 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         L.whist = ws.whist;
         L.went = ws.went;
         L.zero_next = reinterpret_cast<uint32_t *>(&ws.ctl->cc[(a.epoch + 1) & 1u]);
+        if (fused_gather) {  // (fused_gather: bucket 0's gather has a term to add)
+            const GatherArgs &g = *a.b[0].gather;
+            L.gres = g.resid;
+            for (uint32_t x = 1; x < g.nsrc && x < GATHER_MAX; ++x) L.gsrc[x] = g.src[x];
+            L.gn = std::max<uint32_t>(1, g.nsrc);
+            L.tl = (uint32_t)(a.b[0].n % 16);
+        }
         hipError_t e = launch_tv16_lscan(L, a.num_cu, s);
         if (e != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[1], s);

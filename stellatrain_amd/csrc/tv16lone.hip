@@ -112,11 +112,28 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
     if (lane == 0) lds_st(&L.fin[sl], j + 1);
 }
 
-template <bool EF, uint32_t NW, uint32_t D>
+// GS > 0: the gather-add fused into the stream (gather.hip, ModuleCpuGather::run,
+// engine/modules/cpu_gather.cpp:59-87): up to GS more input streams (the
+// residual, then grad[1] .. grad[N-1]) are read beside the bucket, summed into
+// it in gather.hip's order, and the sum is stored back once (grad[0] ends as
+// the gather-add leaves it) and is what the line sums see.
+template <bool EF, uint32_t NW, uint32_t D, uint32_t GS>
 __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
     __shared__ LLds L;
     const uint32_t tid = threadIdx.x;
     if (tid < 2) { L.qn[tid] = 0; L.wn[tid] = 0; L.done[tid] = 0; L.fin[tid] = 0; }
+    // the extra streams in summation order: the residual, then grad[1] ..
+    const uint32_t ns = GS ? (A.gres ? 1u : 0u) + (A.gn ? A.gn - 1u : 0u) : 0u;
+    auto xs = [&](uint32_t e) -> const float * {
+        if (A.gres) return e == 0 ? A.gres : A.gsrc[e];
+        return A.gsrc[e + 1u];
+    };
+    if (GS && blockIdx.x == 0 && tid < A.tl) {  // the ragged tail (the stream covers full lines)
+        const size_t e = (size_t)A.nb * 16 + tid;
+        float acc = A.src[e];
+        for (uint32_t x = 0; x < ns; ++x) acc += xs(x)[e];
+        const_cast<float *>(A.src)[e] = acc;
+    }
     // the next call's counters (the finish of this call uses the other copy)
     if (blockIdx.x == 0 && tid < sizeof(CallCtl) / 4) st_sc1(A.zero_next + tid, 0u);
     const uint32_t s = uni(tid >> 6), lane = flane(), q = lane & 3u;
@@ -149,6 +166,25 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
             return make_float4(__uint_as_float(t4.x), __uint_as_float(t4.y), __uint_as_float(t4.z),
                                __uint_as_float(t4.w));
         };
+        __amdgpu_buffer_rsrc_t rx[GS ? GS : 1];  // extra streams (past ns: no records, reads 0, never added)
+#pragma unroll
+        for (uint32_t e = 0; e < (GS ? GS : 1u); ++e)
+            rx[e] = __builtin_amdgcn_make_buffer_rsrc(e < ns ? const_cast<float *>(xs(e)) + (size_t)L0 * 16 : nullptr, 0,
+                                                      e < ns ? nl * 64u : 0u, 0x00020000);
+        auto load_x = [&](uint32_t e, uint32_t m) -> float4 {
+            uint32_t voff = lane_line * 64u + q * 16u;
+            asm volatile("" : "+v"(voff));
+            const u4v t4 = __builtin_amdgcn_raw_buffer_load_b128(rx[e], voff + m * (NW * 1024u), 0, 2 /* nt */);
+            return make_float4(__uint_as_float(t4.x), __uint_as_float(t4.y), __uint_as_float(t4.z),
+                               __uint_as_float(t4.w));
+        };
+        auto store_s = [&](uint32_t m, float4 x) {  // the gathered sum back into the bucket
+            uint32_t voff = lane_line * 64u + q * 16u;
+            asm volatile("" : "+v"(voff));
+            u4v t4;
+            t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
+            __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc, voff + m * (NW * 1024u), 0, 0);
+        };
         auto store_r = [&](uint32_t m, float4 x) {
             uint32_t voff = lane_line * 64u + q * 16u;
             asm volatile("" : "+v"(voff));
@@ -156,9 +192,13 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
             t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
             __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NW * 1024u), 0, STG_EF_AUX);
         };
-        float4 v[D];
+        float4 v[D], w[GS ? GS : 1][D];
 #pragma unroll
-        for (uint32_t u = 0; u < D; ++u) v[u] = load(u);
+        for (uint32_t u = 0; u < D; ++u) {
+            v[u] = load(u);
+#pragma unroll
+            for (uint32_t e = 0; e < GS; ++e) w[e][u] = load_x(e, u);
+        }
         if (j == 0) {  // the threshold, read while the chunk's first loads are in flight
             t = uni(A.state->t);
             if (blockIdx.x == 0 && tid == 0) {  // the finish decides with the threshold the scan used
@@ -172,7 +212,20 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
         for (uint32_t m0 = 0; m0 < mine; m0 += D) {
 #pragma unroll
             for (uint32_t u = 0; u < D; ++u) {
-                const float4 x = v[u];
+                float4 x = v[u];
+                if (GS) {  // dst + residual + grad[1] + ... in gather.hip's order
+#pragma unroll
+                    for (uint32_t e = 0; e < GS; ++e) {
+                        const float4 y = w[e][u];
+                        const bool on = e < ns;
+                        x.x = on ? x.x + y.x : x.x;
+                        x.y = on ? x.y + y.y : x.y;
+                        x.z = on ? x.z + y.z : x.z;
+                        x.w = on ? x.w + y.w : x.w;
+                        w[e][u] = load_x(e, m0 + u + D);
+                    }
+                    store_s(m0 + u, x);
+                }
                 if (STG_LSCAN_DIAG == 2) {
                     v[u] = load(m0 + u + D);
                     if (__float_as_uint(x.x + x.y + x.z + x.w) == 0x7f800001u) L.qn[sl] = 1;
@@ -248,12 +301,25 @@ hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s) {
     const bool ef = a.resid != nullptr;
     const uint32_t per_cu = shape == 1 ? 4u : 8u;
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(a.nc, per_cu * (uint32_t)num_cu));
-    if (shape == 1) {
-        if (ef) tv16_lscan<true, 8, 4><<<G, 512, 0, s>>>(a);
-        else tv16_lscan<false, 8, 4><<<G, 512, 0, s>>>(a);
+    if (a.gn) {  // the gather fused: fewer loads in flight per stream, more streams
+        const uint32_t ns = (a.gres ? 1u : 0u) + a.gn - 1u;
+        if (a.gn > GATHER_MAX) return hipErrorInvalidValue;
+        if (ns <= 3) {
+            if (ef) tv16_lscan<true, 4, 4, 3><<<G, 256, 0, s>>>(a);
+            else tv16_lscan<false, 4, 4, 3><<<G, 256, 0, s>>>(a);
+        } else if (ns <= 8) {
+            if (ef) tv16_lscan<true, 4, 2, 8><<<G, 256, 0, s>>>(a);
+            else tv16_lscan<false, 4, 2, 8><<<G, 256, 0, s>>>(a);
+        } else {
+            if (ef) tv16_lscan<true, 4, 1, GATHER_MAX><<<G, 256, 0, s>>>(a);
+            else tv16_lscan<false, 4, 1, GATHER_MAX><<<G, 256, 0, s>>>(a);
+        }
+    } else if (shape == 1) {
+        if (ef) tv16_lscan<true, 8, 4, 0><<<G, 512, 0, s>>>(a);
+        else tv16_lscan<false, 8, 4, 0><<<G, 512, 0, s>>>(a);
     } else {
-        if (ef) tv16_lscan<true, 4, 8><<<G, 256, 0, s>>>(a);
-        else tv16_lscan<false, 4, 8><<<G, 256, 0, s>>>(a);
+        if (ef) tv16_lscan<true, 4, 8, 0><<<G, 256, 0, s>>>(a);
+        else tv16_lscan<false, 4, 8, 0><<<G, 256, 0, s>>>(a);
     }
     return hipGetLastError();
 }

@@ -155,6 +155,13 @@ struct DevWS {
 };
 
 // ---- launchers (implemented in the .hip files) ----
+constexpr uint32_t GATHER_MAX = 16;  // local GPUs per node the gather-add accepts
+struct GatherArgs {
+    float *dst;                    // grad[0]
+    const float *resid;            // residual (or null: no residual term)
+    const float *src[GATHER_MAX];  // src[1 .. nsrc-1] = grad[1 .. N-1]; src[0] unused
+    uint32_t nsrc;                 // N, the node's GPU count
+};
 struct Tv16Bucket {
     const float *src;
     size_t n;
@@ -169,6 +176,7 @@ struct Tv16Bucket {
     float *sums;       // per-bucket scratch: first-threshold line sums; the fill's candidate heap
                        // (2 words per line: (nb + 1) * 2 floats)
     float *resid;      // MERGE error feedback: receives the bucket's full lines, or null
+    const GatherArgs *gather;  // intra-node gather-add fused into the scan (dst = src), or null
 };
 struct Tv16Launch {
     const Tv16Bucket *b;
@@ -242,6 +250,12 @@ struct LScanArgs {
     uint32_t *whist;       // window entries per bin (zero at the start of the call)
     uint2 *went;           // ... and the entries, LBCAP per bin
     uint32_t *zero_next;   // the next call's counter block (CallCtl), zeroed here
+    // the gather-add fused into the stream (gather.hip's sum, in its order):
+    // src += gres + gsrc[1] + ... + gsrc[gn - 1], stored back to src once
+    const float *gres;     // residual term (null: none)
+    const float *gsrc[GATHER_MAX];
+    uint32_t gn;           // 0: no gather; else N (gsrc[0] unused)
+    uint32_t tl;           // the ragged tail's floats (summed by workgroup 0)
 };
 hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s);
 
@@ -348,13 +362,6 @@ struct AdamLaunch {
 };
 constexpr uint32_t ADAM_TILE = STG_WG * 4;  // amsgrad: elements per workgroup tile
 hipError_t launch_adam(const AdamLaunch &a, hipStream_t s);
-constexpr uint32_t GATHER_MAX = 16;  // local GPUs per node the gather-add accepts
-struct GatherArgs {
-    float *dst;                    // grad[0]
-    const float *resid;            // residual (or null: no residual term)
-    const float *src[GATHER_MAX];  // src[1 .. nsrc-1] = grad[1 .. N-1]; src[0] unused
-    uint32_t nsrc;                 // N, the node's GPU count
-};
 hipError_t launch_gather_add(const GatherArgs &a, size_t start, size_t end, int num_cu, hipStream_t s);
 constexpr uint32_t WIRE_BATCH = 16;  // buckets per batched wire launch
 struct WireBucket {

@@ -466,6 +466,57 @@ def gather(torch, calls):
     return out
 
 
+def gather_fused(torch, calls):
+    """One MERGE task with the intra-node gather ahead of it on a 64 MiB
+    bucket (cpu_gather.cpp:59-87 then compress.cpp:139-186):
+    stg_merge_gather_compress_device (thresholdv16 sums the N - 1 sources and
+    the residual inside its streaming pass) against the gather-add pass then
+    the fused MERGE compress (stg_merge_compress_batch_device).  Every step
+    regenerates grad[0] and the residual (two alternating inputs); the fill
+    alone is timed and subtracted.  Alg. bytes (fused): 4n (N + 1)
+    read + 8n written (grad[0], residual) + 8k."""
+    from stellatrain_amd import ThresholdvCompressor16, gather_add, merge_numel
+    from stellatrain_amd._capi import lib
+    from stellatrain_amd.synth import seed_for
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    n = 16 << 20
+    k = merge_numel(n, 0.99)
+    out = []
+    for g in (2, 4, 8):
+        srcs = bufs_for(torch, lib(), dev, n, g + 1, st.cuda_stream, 700)
+        grads, resid = srcs[:g], srcs[g]
+        idx = torch.zeros(k, dtype=torch.int32, device=dev)
+        val = torch.zeros(k, dtype=torch.float32, device=dev)
+        counts = torch.zeros(1, dtype=torch.int32, device=dev)
+        row = {"config": f"GATHER + MERGE compress (EF), thresholdv16 64 MiB k={k}, N={g} sources + residual"}
+        for fused in (True, False):
+            comp = ThresholdvCompressor16()
+
+            def step(s, run=True):
+                # two alternating inputs (as the headline's two buffer sets): the
+                # key's threshold settles as it does in training
+                fill(lib(), grads[0], seed_for(700, s % 2), st.cuda_stream)
+                fill(lib(), resid, seed_for(760, s % 2), st.cuda_stream)  # (no collision with grad[1..])
+                if not run:
+                    return
+                if fused:
+                    comp.merge_gather_compress_async("gf@w", grads, k, idx, val, residual=resid, count=counts)
+                else:
+                    for r in range(g):  # every rank's slice of the bucket: the whole bucket
+                        gather_add(grads, resid, r)
+                    comp.compress_batch_async([("gf@w", grads[0], k, idx, val)], counts=counts, residuals=[resid])
+            us = _time_loop(torch, st, step, calls, 4) - _time_loop(torch, st, lambda s: step(s, False), calls, 2)
+            row["fused_us" if fused else "separate_us"] = round(us, 2)
+            if fused:
+                alg = 4.0 * n * (g + 1) + 8.0 * n + 8.0 * k
+                row["fused_alg_GBps"] = round(alg / us / 1e3, 1)
+                row["fused_frac"] = round(alg / us / 1e3 / PEAK, 3)
+        out.append(row)
+        del srcs, grads, resid
+    return out
+
+
 def cpu_codec(method, mib, ratio, seconds):
     """The reference CPU path beside its GPU row, same run, this host's cores
     (north_star): oracle/_ref/libstg_ref.so (the reference's compress/*.cpp
@@ -536,7 +587,7 @@ def main():
     p.add_argument("--calls", type=int, default=48)
     p.add_argument("--c4-streams", type=int, default=4)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU baseline row (0: none)")
-    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,merge,ef,gather")
+    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,merge,ef,gather,gfused")
     a = p.parse_args()
     import torch
     from stellatrain_amd import make_compressor
@@ -563,6 +614,9 @@ def main():
     if "c5" in only:
         for kind in ("sgd", "sgd_fused", "adam", "adam_fused", "adam_ams"):
             emit(c5_round_trip(torch, a.calls, kind))
+    if "gfused" in only:
+        for r in gather_fused(torch, a.calls):
+            emit(r)
     if "gather" in only:
         for d in gather(torch, a.calls):
             emit(d)
