@@ -582,14 +582,19 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     __syncthreads();
     TopkCtl *const C = A.ctl;
     if (blockIdx.x == 0) TK1_STAMP(40);
-    {   // the next call's control block and band histogram, in shares (this call never touches them)
+    // the next call's control block and band histogram, zeroed in shares
+    // (this call never touches them) with plain stores at the workgroup's end:
+    // vmcnt counts stores with loads, in order, so stores issued first would
+    // hold this workgroup's later loads (the next call's launches see them
+    // after this kernel's end)
+    auto zero_next = [&]() {
         constexpr uint32_t CW = (uint32_t)(sizeof(TopkCtl) / 16), FW = TK2_FINE / 4u;
+        uint4 *const c4 = reinterpret_cast<uint4 *>(A.ctl_next), *const f4 = reinterpret_cast<uint4 *>(A.fine_next);
         for (uint32_t i = blockIdx.x * STG_WG + tid; i < CW + FW; i += gridDim.x * STG_WG) {
-            if (i < CW) st_sc1_zero16(reinterpret_cast<uint32_t *>(A.ctl_next), (uint32_t)sizeof(TopkCtl), 16u * i);
-            else st_sc1_zero16(A.fine_next, TK2_FINE * 4u, 16u * (i - CW));
+            if (i < CW) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+            else f4[i - CW] = make_uint4(0u, 0u, 0u, 0u);
         }
-    }
-    if (blockIdx.x == 0) TK1_STAMP(41);  // workgroup 0: zeroing done
+    };
     const uint32_t home = blockIdx.x % TK1_SH;
     auto poison = [&]() {
         if (tid == 0) {
@@ -599,6 +604,11 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     };
     // the band's way
     Pick P;
+    // the hit path's NU emission units: the first NU workgroups take one
+    // ticket each (units in ticket order), issued before the pick so its
+    // round trip overlaps the pick's loads
+    const uint32_t NU = (A.nt + A.ut - 1u) / A.ut;
+    if (tid == 0) L.v[9] = blockIdx.x < NU ? g_add(&C->utk[0], 1u) : NU;
     const bool hit = !A.force_miss && pick_exact(A, L, P);
     if (blockIdx.x == 0) TK1_STAMP(42);  // workgroup 0: pick done
     TK1_STAMP_MAX(43);                   // every workgroup's pick done
@@ -610,19 +620,16 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
             atomicAdd(&A.dbg[38], 1u);
         }
         const uint64_t need_eq = (uint64_t)A.k - P.gt;
-        const uint32_t NU = (A.nt + A.ut - 1u) / A.ut;
-        if (blockIdx.x >= NU) return;  // NU workgroups take the units (NU tickets on the counter word)
-        for (;;) {
-            if (tid == 0) L.v[9] = ld_sc1(&C->utk[0]) >= NU ? NU : g_add(&C->utk[0], 1u);
-            __syncthreads();
-            const uint32_t u = L.v[9];
-            __syncthreads();
-            if (u >= NU) break;
+        __syncthreads();
+        const uint32_t u = L.v[9];
+        __syncthreads();
+        if (u < NU) {
             TK1_STAMP_MAX(48);  // the last unit taken
-            if (!emit_unit(A, L, u, P.T, need_eq)) { poison(); return; }
+            if (!emit_unit(A, L, u, P.T, need_eq)) { poison(); zero_next(); return; }
             TK1_STAMP_MAX(44);  // the last unit done
         }
         TK1_STAMP_MAX(45);      // the last workgroup out
+        zero_next();
         return;
     }
     if (blockIdx.x == 0 && tid == 0 && ld_sc1(&C->band_ok)) {  // a hinted call missed: widen the band
@@ -706,7 +713,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     const uint32_t seq[4] = {M_H1, M_H2, M_H3, M_CNT};
     for (uint32_t i = 0; i < 4; ++i) {
         run_multi(seq[i], 0, 0);
-        if (!wait_flag(seq[i] + 1u)) { poison(); return; }
+        if (!wait_flag(seq[i] + 1u)) { poison(); zero_next(); return; }
     }
     const uint32_t T = ld_sc1(&C->res_T);
     const uint64_t tgt = ld_sc1(&A.tile_gt[2 * A.nt]), teq = ld_sc1(&A.tile_eq[2 * A.nt]);
@@ -720,6 +727,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         }
     }
     run_multi(P_EMIT, T, need_eq);
+    zero_next();
 }
 
 }  // namespace
@@ -786,7 +794,8 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     A.ut = std::max(1u, std::min(A.ut, TK2_UT));
     A.fine_next = ws.tkfine + (size_t)((tag + 1u) & 1u) * TK2_FINE;
     A.dbg = ws.misc;
-    const uint32_t G = std::min<uint32_t>(nt, (uint32_t)a.num_cu * 2u);
+    // every emission unit has a workgroup of its own (NU <= TK2_UNITS)
+    const uint32_t G = std::max<uint32_t>(std::min<uint32_t>(nt, (uint32_t)a.num_cu * 2u), (nt + A.ut - 1u) / A.ut);
     static const int dbg_mode = getenv("STG_TK1_DEBUG") ? atoi(getenv("STG_TK1_DEBUG")) : 0;
     A.force_miss = dbg_mode == 2;
     if (vec) tk_one<true><<<G, STG_WG, 0, s>>>(A);
