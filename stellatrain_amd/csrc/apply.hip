@@ -475,10 +475,11 @@ __global__ void __launch_bounds__(STG_WG) win_emit1t(Win1Args a) {
         for (uint32_t i0 = 0; i0 < tile; i0 += STG_WG) {
             const uint32_t i = i0 + tid;
             uint64_t d = i < tile ? ld_sc1(&a.desc[i]) : 0ull;
+            uint64_t st = 0;
             for (uint32_t spins = 0; i < tile && (uint32_t)(d >> 32) != a.tag; ++spins) {
                 __builtin_amdgcn_s_sleep(4);
                 d = ld_sc1(&a.desc[i]);
-                if (spins > (1u << 20)) { gave = true; break; }  // ~0.3 s: give up, poison the count
+                if (spin_expired(spins, st)) { gave = true; break; }  // 200 ms: give up, poison the count
             }
             Pl += (uint32_t)d;
         }
@@ -689,8 +690,9 @@ __global__ void __launch_bounds__(STG_WG) adam_apply_ams(AdamLaunch a, uint32_t 
         uint32_t pt = vmax0;
         for (uint32_t p = threadIdx.x; p < tile; p += STG_WG) {
             uint64_t w = ld_sc1(&words[p]);
+            uint64_t st = 0;
             for (uint32_t spins = 0; (uint32_t)(w >> 32) != tag; ++spins) {
-                if (spins >= (1u << 22)) {  // starved predecessor: flag it (stg_adam_check), never use a stale word silently
+                if (spin_expired(spins, st)) {  // starved predecessor: flag it (stg_adam_check), never use a stale word silently
                     g_or(a.fail, FAIL_SPIN_TIMEOUT);
                     break;
                 }

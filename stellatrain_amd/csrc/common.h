@@ -191,79 +191,16 @@ __device__ __forceinline__ uint32_t g_or(uint32_t *p, uint32_t v) {
     return __hip_atomic_fetch_or(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Fence-free grid barrier for sc1/atomic-only hand-offs: every wave drains its
-// stores, one lane adds to a monotonic counter (zeroed before use), polls it
-// relaxed with s_sleep until `target`, bounded.
-__device__ __forceinline__ void grid_barrier_sc1(uint32_t *ctr, uint32_t target, uint32_t *fail) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t spins = 0;
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 24)) { atomicOr(fail, 1u /*FAIL_SPIN_TIMEOUT*/); break; }
-        }
-    }
-    __syncthreads();
-}
-
-// --- inter-workgroup hand-off (MI355X_MICROARCH "Valid forms", cdna_hip
-//     Guideline 16): producer = every wave drains, barrier, one lane releases
-//     at agent scope then bumps a relaxed agent counter; consumer = one lane
-//     polls relaxed with s_sleep (bounded), one agent acquire, barrier. ---
-__device__ __forceinline__ uint32_t ld_acq_relaxed(const uint32_t *p) {
-    return __hip_atomic_load(gp(const_cast<uint32_t *>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void release_prologue() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-}
-
-// Arrive on a monotonic counter; the caller's lane 0 returns the old value.
-__device__ __forceinline__ uint32_t arrive(uint32_t *ctr) {
-    release_prologue();
-    uint32_t old = 0;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return old;
-}
-
-// Grid barrier on a monotonic counter zeroed before the launch: the b-th
-// barrier (1-based) waits until the counter reaches b * nwg.  Bounded spin.
-__device__ __forceinline__ void grid_barrier(uint32_t *ctr, uint32_t target, uint32_t *fail) {
-    __shared__ uint32_t s_ok;
-    arrive(ctr);
-    if (threadIdx.x == 0) {
-        uint32_t spins = 0;
-        uint32_t ok = 1;
-        while (ld_acq_relaxed(ctr) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) { ok = 0; atomicOr(fail, (uint32_t)FAIL_SPIN_TIMEOUT); break; }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_ok = ok;
-    }
-    __syncthreads();
-    (void)s_ok;
-}
-
-// Wave-aggregated append to a global counter: returns this lane's slot.
-__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool pred) {
-    const uint64_t m = __ballot(pred);
-    const uint32_t lane = __lane_id();
-    const uint32_t nb = __popcll(m);
-    const uint32_t leader = m ? (uint32_t)__ffsll((long long)m) - 1u : 0u;
-    uint32_t base = 0;
-    if (m && lane == leader) base = atomicAdd(ctr, nb);
-    base = __shfl(base, (int)leader, 64);
-    const uint32_t below = __popcll(m & ((1ull << lane) - 1ull));
-    return base + below;
+// Bounded waits give up after SPIN_TICKS of the 100 MHz s_memrealtime clock
+// (read every 64 polls, from the first poll on): the same wall-clock limit at
+// every site, whatever one poll costs (a poll is a memory round trip, so a
+// bound counted in polls can run for seconds).
+constexpr uint64_t SPIN_TICKS = 20000000;  // 200 ms
+__device__ __forceinline__ bool spin_expired(uint32_t spins, uint64_t &t0) {
+    if (spins & 63u) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (spins == 0) { t0 = now; return false; }
+    return now - t0 > SPIN_TICKS;
 }
 
 }  // namespace stg

@@ -217,10 +217,11 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     bool gave_up = false;
     if (tid < r) {
         uint64_t d = ld_sc1(&a.desc[tid]);
+        uint64_t st = 0;
         for (uint32_t spins = 0; (uint32_t)(d >> 32) != a.tag; ++spins) {
             __builtin_amdgcn_s_sleep(8);
             d = ld_sc1(&a.desc[tid]);
-            if (spins > (1u << 20)) { gave_up = true; break; }  // ~0.5 s: the count is poisoned below
+            if (spin_expired(spins, st)) { gave_up = true; break; }  // 200 ms: the count is poisoned below
         }
         Pl = (uint32_t)d;
     }
@@ -293,10 +294,11 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     uint32_t gm = 0;
     for (uint32_t i = tid; i < G; i += TWG) {  // every range's tagged maximum
         uint64_t x = ld_sc1(&a.rmax[i]);
+        uint64_t st = 0;
         for (uint32_t spins = 0; (uint32_t)(x >> 32) != a.tag; ++spins) {
             __builtin_amdgcn_s_sleep(8);
             x = ld_sc1(&a.rmax[i]);
-            if (spins > (1u << 20)) { g_or(a.fail, FAIL_SPIN_TIMEOUT); break; }
+            if (spin_expired(spins, st)) { g_or(a.fail, FAIL_SPIN_TIMEOUT); break; }
         }
         gm = max(gm, (uint32_t)x);
     }

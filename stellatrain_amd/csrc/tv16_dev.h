@@ -11,16 +11,7 @@ namespace tv16 {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
-// Bounded waits give up after SPIN_TICKS of the 100 MHz s_memrealtime clock
-// (read every 64 polls, from the first poll on): the same wall-clock limit at
-// every site, so the wait that started first also gives up first.
-constexpr uint64_t SPIN_TICKS = 20000000;  // 200 ms
-__device__ __forceinline__ bool spin_expired(uint32_t spins, uint64_t &t0) {
-    if (spins & 63u) return false;
-    const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (spins == 0) { t0 = now; return false; }
-    return now - t0 > SPIN_TICKS;
-}
+using ::stg::spin_expired;  // common.h: every bounded wait gives up after 200 ms
 
 __device__ __forceinline__ uint32_t bitlen(uint32_t x) { return x ? 32u - __clz(x) : 0u; }
 
