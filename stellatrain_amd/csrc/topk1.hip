@@ -12,7 +12,7 @@
 // a band [F, H) = T_prev (1 -/+ d), at most TK2_FINE ulps wide, that almost
 // always holds this call's T.  Two launches:
 //   tk2_stream  one workgroup per 32 KiB tile, no waits: the tile's superset
-//               {|x| >= F} (in index order) into region tile % 8 at an offset
+//               {|x| >= F} (in index order) into region tile % 32 at an offset
 //               taken by one atomic; its count of keys >= H; every band key
 //               into the band histogram, one bin per ulp (and a coarse one per
 //               256 ulps).  One read of the bucket.
@@ -68,6 +68,13 @@ constexpr float D_SEED = 1.0f / 256.0f;  // ... after a key's first call
 
 __device__ __forceinline__ uint32_t mag1(uint32_t bits) { return bits & 0x7fffffffu; }
 
+// Coarse bin c's word: bins interleaved over 64 lines of 16 words (c mod 64
+// picks the line), so the few dozen bins a narrow band covers sit on as many
+// lines -- consecutive bins on one 128-byte line serialise every tile's band
+// atomics at that line.
+__device__ __forceinline__ uint32_t coarse_word(uint32_t c) { return (c & 63u) * 16u + (c >> 6); }
+static_assert(TK2_COARSE == 1024, "64 lines x 16 words");
+
 // The band of this call from the key's hint: [F, H) in key bits, at most
 // TK2_FINE wide (centred on T_prev when d T_prev spans more ulps); ok = false
 // for a hint that cannot steer (zero, denormal, inf or NaN).
@@ -93,12 +100,6 @@ __device__ __forceinline__ Band band_of(const KeyState *st) {
 // ---------------------------------------------------------------------------
 // the stream launch
 // ---------------------------------------------------------------------------
-#ifndef STG_TK2_NOATOM
-#define STG_TK2_NOATOM 0  // experiment: no band histogram (results wrong)
-#endif
-#ifndef STG_TK2_FIXED
-#define STG_TK2_FIXED 0   // experiment: fixed per-tile superset slots instead of an offset atomic
-#endif
 struct T2Stream {
     const float *a;
     uint64_t m;
@@ -106,9 +107,9 @@ struct T2Stream {
     const KeyState *state;
     TopkCtl *ctl;
     uint32_t *fine;        // this call's band histogram (TK2_FINE words, zero)
-    uint2 *sup;            // superset regions: TK1_SH of shard_cap entries {element, bits}
+    uint2 *sup;            // superset regions: TK2_REG of shard_cap entries {element, bits}
     uint32_t shard_cap;
-    uint32_t *sup_n, *sup_off;  // per tile: superset entries, offset in region tile % 8
+    uint32_t *sup_n, *sup_off;  // per tile: superset entries, offset in region tile % TK2_REG
     uint32_t *count_out;
     uint32_t cap;
 };
@@ -141,10 +142,10 @@ __global__ void __launch_bounds__(STG_WG) tk2_stream(const T2Stream A) {
                 q |= 1u << (u * 4 + j);
                 if (key >= B.H) {
                     ++nhi;
-                } else if (!STG_TK2_NOATOM) {
+                } else {
                     const uint32_t f = key - B.F;
                     __hip_atomic_fetch_add(gp(&A.fine[f]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(gp(&A.ctl->coarse[f >> TK2_CSH]), 1u, __ATOMIC_RELAXED,
+                    __hip_atomic_fetch_add(gp(&A.ctl->coarse[coarse_word(f >> TK2_CSH)]), 1u, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
@@ -166,13 +167,10 @@ __global__ void __launch_bounds__(STG_WG) tk2_stream(const T2Stream A) {
         if (tid == NW - 1) s_wt[NW] = inc;
     }
     __syncthreads();
-    const uint32_t nsup = s_wt[TILE_U * STG_WAVES], sh = tile % TK1_SH;
+    const uint32_t nsup = s_wt[TILE_U * STG_WAVES], sh = tile % TK2_REG;
     if (tid == 0) {
         uint32_t off = 0;
-        if (STG_TK2_FIXED) {
-            off = (tile / TK1_SH) * TOPK_SUP_CAP;
-            if (nsup > TOPK_SUP_CAP) { A.ctl->ovf = 1u; off = A.shard_cap; }
-        } else if (nsup) {
+        if (nsup) {
             off = g_add(&A.ctl->shn[sh][0], nsup);
             if (off + nsup > A.shard_cap) A.ctl->ovf = 1u;
         }
@@ -267,7 +265,7 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
     uint32_t c[PER], s = 0, hi = tid < TK2_HI ? C->hi[tid][0] : 0u;
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {  // top-down: thread tid holds coarse bins 1023 - (PER tid + j)
-        c[j] = C->coarse[TK2_COARSE - 1u - (PER * tid + j)];
+        c[j] = C->coarse[coarse_word(TK2_COARSE - 1u - (PER * tid + j))];
         s += c[j];
     }
     uint32_t th, tband;
@@ -318,7 +316,7 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
         const bool bad = tid < nT && (c > TV_TILE || o + c > A.shard_cap);
         if (tid <= TK2_UT) L.up[tid] = tid < nT ? ex : 0xffffffffu;
         // entry f of tile j is at sup[ub[j] + f] (mod 2^32: the true index is < 2^32)
-        if (tid < nT) L.ub[tid] = ((t0 + tid) % TK1_SH) * A.shard_cap + o - ex;
+        if (tid < nT) L.ub[tid] = ((t0 + tid) % TK2_REG) * A.shard_cap + o - ex;
         const uint32_t tot = __shfl(incl, (int)nT - 1, 64);
         if (tid == nT) L.up[tid] = tot;
         const uint64_t b = __ballot(bad);
@@ -752,8 +750,8 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     }
     TopkCtl *const ctl = ws.tkctl + (tag & 1u);
     uint32_t *const fine = ws.tkfine + (size_t)(tag & 1u) * TK2_FINE;
-    // superset regions: the bucket's share of TOPK_SUP_CAP entries per tile, in TK1_SH regions
-    const uint32_t shard_cap = (uint32_t)((size_t)nt * TOPK_SUP_CAP / TK1_SH);
+    // superset regions: the bucket's share of TOPK_SUP_CAP entries per tile, in TK2_REG regions
+    const uint32_t shard_cap = (uint32_t)((size_t)nt * TOPK_SUP_CAP / TK2_REG);
     uint32_t *const sup_n = ws.tile_cnt + 2 * (size_t)nt + 1, *const sup_off = ws.tile_aux + 2 * (size_t)nt + 1;
     uint2 *const sup = reinterpret_cast<uint2 *>(ws.sums);
     const bool vec = (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0;

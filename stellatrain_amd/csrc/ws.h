@@ -113,6 +113,7 @@ constexpr uint32_t TK2_FINE = 1u << 18;               // band bins: one per ulp
 constexpr uint32_t TK2_CSH = 8;                       // coarse bins: 256 ulps
 constexpr uint32_t TK2_COARSE = TK2_FINE >> TK2_CSH;  // 1024
 constexpr uint32_t TK2_HI = 16;                       // shards of the count of keys above the band
+constexpr uint32_t TK2_REG = 32;                      // superset regions (tile mod 32), an offset counter each
 constexpr uint32_t TK2_UT = 16;                       // tiles per emission unit
 constexpr uint32_t TK2_UNITS = TOPK_LIST_TILES / TK2_UT;
 struct alignas(128) TopkCtl {
@@ -124,7 +125,7 @@ struct alignas(128) TopkCtl {
     uint32_t pad[TK1_LINE - TK1_NPH - 5];
     uint32_t utk[TK1_LINE];                    // emission units taken
     uint32_t hi[TK2_HI][TK1_LINE];             // keys >= H, by tile % TK2_HI
-    uint32_t shn[TK1_SH][TK1_LINE];            // superset entries placed in region tile % 8
+    uint32_t shn[TK2_REG][TK1_LINE];           // superset entries placed in region tile % TK2_REG
     uint32_t coarse[TK2_COARSE];               // band keys per 256 ulps
     uint64_t udesc[TK2_UNITS];                 // emission unit u: bit 63 | > T count << 32 | == T count
 };
