@@ -445,7 +445,7 @@ struct TkArgs {
 // stream with STG_OK.
 __device__ __forceinline__ void select_broken(const TkArgs &a) {
     g_or(a.fail, FAIL_SELECT);
-    st_sc1(a.count_out, POISON_COUNT);
+    __hip_atomic_fetch_max(gp(a.count_out), POISON_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One workgroup per tile: the winners (> T, then == T in index order until
@@ -549,7 +549,8 @@ __global__ void __launch_bounds__(STG_WG) tk_emit2(TkArgs a) {
         if (!(ld_sc1(a.fail) & FAIL_SELECT)) {
             st_sc1(a.count_out, a.cap);
             __builtin_amdgcn_s_waitcnt(0);
-            if (ld_sc1(a.fail) & FAIL_SELECT) st_sc1(a.count_out, POISON_COUNT);
+            if (ld_sc1(a.fail) & FAIL_SELECT)  // (POISON_COUNT is the largest value: whichever store lands last, it stays)
+                __hip_atomic_fetch_max(gp(a.count_out), POISON_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -368,7 +368,7 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
     static_assert(PB == 2 && NBIN == LNBIN, "two bins per thread");
     uint32_t h[PB];  // the scan's window entries per bin, in flight with the prefix's loads
 #pragma unroll
-    for (uint32_t u = 0; u < PB; ++u) h[u] = A.whist[PB * tid + u];
+    for (uint32_t u = 0; u < PB; ++u) h[u] = A.whist[whist_word(PB * tid + u)];
     lfin_prefix(L, A, D);
     LF_STAMP(1);
     if (!D.regimeB || (!D.M && !D.tail_cand)) return;  // nothing to fill

@@ -74,7 +74,7 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
     uint32_t wbin = 0, wslot = LBCAP;
     if (lane < wlc) {
         wbin = (tb - 1u - (uint32_t)(we >> 32)) >> 8;  // < LNBIN: the sum is in [t - 2^18 ulps, t)
-        wslot = g_add(&A.whist[wbin], 1u);
+        wslot = g_add(&A.whist[whist_word(wbin)], 1u);
     }
     uint32_t *lq = A.lq + (size_t)c * LQCAP;
     uint2 *lw = A.lw + (size_t)c * LWCAP;

@@ -94,6 +94,11 @@ constexpr uint32_t LMAXC = 4096;  // chunks of a bucket the one-bucket path take
 // the counts are zeroed by the finish's last workgroup after use
 constexpr uint32_t LNBIN = 1024;
 constexpr uint32_t LBCAP = 32;
+// bin b's count word: bins interleaved over 32 lines (b mod 32 picks the
+// line), so the bins the window fills near t sit on as many 128-byte lines
+// (the scan's returning atomics on one line queue behind each other)
+__host__ __device__ constexpr uint32_t whist_word(uint32_t b) { return (b & 31u) * 32u + (b >> 5); }
+static_assert(LNBIN == 1024, "32 lines x 32 words");
 
 // thresholdv16 regime-B crew (tv16wide.h): per bucket slot of a launch, the
 // level-1 histogram of the candidates' keys and the hand-offs between phases
