@@ -543,7 +543,7 @@ tv16_fill(Tv16FillArgs A) {
     __shared__ uint32_t s_role, s_last;
     const uint32_t tid = threadIdx.x;
     if (!LONE && blockIdx.x >= A.nbk) {  // the crew (tv16wide.h)
-        crew_from_decisions(*reinterpret_cast<WideLds *>(fill_lds), S, A);
+        crew_from_decisions<LONE>(*reinterpret_cast<WideLds *>(fill_lds), S, A);
         return;
     }
     uint32_t role = 0;
@@ -553,7 +553,7 @@ tv16_fill(Tv16FillArgs A) {
         role = s_role;
     }
     if (LONE && !A.lfin && role > A.helpers) {  // the crew of a lone launch with helpers
-        crew_from_decisions(*reinterpret_cast<WideLds *>(fill_lds), S, A);
+        crew_from_decisions<LONE>(*reinterpret_cast<WideLds *>(fill_lds), S, A);
         return;
     }
     // lfin (tv16lfin.h): tickets [0, workers) finish the scan, the next

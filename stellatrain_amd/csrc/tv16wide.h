@@ -60,7 +60,8 @@ constexpr uint32_t WRFD = 27;     // rf32: heap positions < 2^28 - 1
 constexpr uint32_t CW_LA = 2048;  // crew phase A: lines per unit at least (128 KiB)
 constexpr uint32_t CW_LC = 8192;  // crew phase C: keys per unit (16 per thread)
 constexpr uint32_t CW_NE = 32;    // crew phase E: emission units
-constexpr uint32_t CW_DA = 6;     // crew phase A: float4 loads in flight per lane
+constexpr uint32_t CW_DA = 6;     // crew phase A: float4 loads in flight per lane (batched fill launches)
+constexpr uint32_t CW_DA_LONE = 12;  // ... one-bucket launches
 constexpr uint32_t CW_PH = 5;     // phases Z A C D E
 constexpr uint32_t LNONE = 0x7fffffffu;
 #ifndef STG_CREW_STAMPS
@@ -737,6 +738,7 @@ __device__ __forceinline__ CrewMap crew_map(const CrewBk &B) {
 }
 
 // A: one unit of la lines.
+template <uint32_t DA>
 __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, uint32_t u) {
     u = uni(u);  // (a callee's arguments arrive in VGPRs)
     ctl = uni_ptr(ctl);
@@ -760,14 +762,14 @@ __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
         const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 2 /* nt */);
         return make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w));
     };
-    float4 v[CW_DA];
+    float4 v[DA];
 #pragma unroll
-    for (uint32_t j = 0; j < CW_DA; ++j) v[j] = load(j);
-    for (uint32_t m0 = 0; m0 < mine; m0 += CW_DA) {
+    for (uint32_t j = 0; j < DA; ++j) v[j] = load(j);
+    for (uint32_t m0 = 0; m0 < mine; m0 += DA) {
 #pragma unroll
-        for (uint32_t j = 0; j < CW_DA; ++j) {
+        for (uint32_t j = 0; j < DA; ++j) {
             const float4 x = v[j];
-            v[j] = load(m0 + j + CW_DA);
+            v[j] = load(m0 + j + DA);
             if (m0 + j >= mine) continue;
             const uint32_t s = wave + (m0 + j) * FNW_F, line = s * 16u + (lane >> 2);
             const float S = quad_line_sum(x);
@@ -919,6 +921,9 @@ __device__ __forceinline__ uint32_t phase_units(const CrewBk &B, uint32_t p) {
     return p == 1 ? B.nA : p == 2 ? B.nC : p == 4 ? CW_NE : 1u;
 }
 
+// LONE: a one-bucket fill launch (one workgroup per CU, the kernel's register
+// budget is not shared with scans): phase A keeps twice the loads in flight
+template <bool LONE>
 __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A) {
     const uint32_t tid = threadIdx.x;
     CallCtl *const cc = A.cc;
@@ -952,7 +957,7 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
                 st_sc1_zero16(ctl->hist, WBINS * 4u, 16u * i);
             if (tid == 0) st_sc1(&ctl->status, 0u);
         } else if (p == 1) {  // A
-            crew_a(W, B, ctl, rel);
+            crew_a<LONE ? CW_DA_LONE : CW_DA>(W, B, ctl, rel);
         } else if (p == 2) {  // C
             if (!crew_c(W, B, ctl, rel, A.epoch)) { poison(); return; }
         } else if (p == 3) {  // D: the leader, or the literal heap
@@ -1053,6 +1058,7 @@ __device__ __forceinline__ void crew_plan(WideLds &W, uint32_t ncrew) {
 // A crew workgroup of a batched launch (or a lone one with helpers): the
 // launch's window-miss buckets, from the scan's decisions (final: the scan
 // launch has ended).
+template <bool LONE>
 __device__ __forceinline__ void crew_from_decisions(WideLds &W, FillLds &S, const Tv16FillArgs &A) {
     if (threadIdx.x == 0) {
         uint32_t nr = 0;
@@ -1079,7 +1085,7 @@ __device__ __forceinline__ void crew_from_decisions(WideLds &W, FillLds &S, cons
     __syncthreads();
     if (!W.nreq) return;
     crew_plan(W, A.crew);
-    crew_loop(W, S, CrewArgs{A.cc, A.fail, A.dbg, A.crew_ctl, A.epoch});
+    crew_loop<LONE>(W, S, CrewArgs{A.cc, A.fail, A.dbg, A.crew_ctl, A.epoch});
 }
 
 // A crew workgroup of a one-bucket (lfin) launch: the decision every lfin role
@@ -1109,5 +1115,5 @@ __device__ __forceinline__ void crew_lfin(LfinLds &Lf, const Tv16FillArgs &A) {
     __syncthreads();
     if (!W.nreq) return;
     crew_plan(W, A.crew);
-    crew_loop(W, *reinterpret_cast<FillLds *>(&Lf), CrewArgs{A.cc, A.fail, A.dbg, A.crew_ctl, A.epoch});
+    crew_loop<true>(W, *reinterpret_cast<FillLds *>(&Lf), CrewArgs{A.cc, A.fail, A.dbg, A.crew_ctl, A.epoch});
 }
