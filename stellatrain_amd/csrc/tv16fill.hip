@@ -1254,7 +1254,7 @@ tv16_fill(Tv16FillArgs A) {
 
 }  // namespace
 
-constexpr size_t LFIN_LDS = sizeof(FillLds) > sizeof(LfinLds) ? sizeof(FillLds) : sizeof(LfinLds);
+constexpr size_t LFIN_LDS = std::max(std::max(sizeof(FillLds), sizeof(LfinLds)), sizeof(WideLdsBig));
 static_assert(LFIN_LDS <= 160 * 1024, "one lfin workgroup per CU");
 
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {

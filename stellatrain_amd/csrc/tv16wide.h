@@ -76,13 +76,23 @@ struct CrewBk {
     uint32_t la, nA, nC;  // A: lines per unit, units; C: units
 };
 
-// LDS of the leader and the crew (a view of the fill launch's dynamic LDS).
-struct WideLds {
+// LDS of the leader and the crew (a view of the fill launch's dynamic LDS):
+// WT entries of R ranked per tile, NBH bins while sorting.  The batched fill
+// launch shares its CU with two scan workgroups (WideLds: 4,096 / 8,192); the
+// one-bucket (lfin) launch has the CU to itself, so its crew ranks 11,264
+// entries per tile (the 10.5 k pops of a 64 MiB bucket in one pass over the
+// list) with 4,096 bins (WideLdsBig, ~153 KB).
+template <uint32_t WT_, uint32_t NBH_>
+struct WideLdsT {
+    static constexpr uint32_t WT = WT_, NBH = NBH_;
+    static_assert(NBH >= 2048 && (NBH & (NBH - 1u)) == 0 && NBH <= WBINS, "sort bins");
+    static_assert(WT <= 2u * (WSIM + 1u), "the late-line list fits the replay's LDS");
     union {
+        uint32_t hist8[WBINS];     // the crew's phases: level-1 bins, the emission shares' positions
         struct {
-            uint32_t hist[WBINS];  // bins (select, sort, crew phase A)
-            uint64_t tk[WTILE];    // ranking tile: composite keys
-            uint32_t ti[WTILE];    // ... their list entries
+            uint32_t hist[NBH];    // bins (select, sort)
+            uint64_t tk[WT];       // ranking tile: composite keys (the run reorder: two words of each entry)
+            uint32_t ti[WT];       // ... their list entries
         } s;
         uint2 sim[WSIM + 1];       // a replayed subtree: {ordered key (0: -inf), list entry}
     } u;
@@ -95,7 +105,11 @@ struct WideLds {
     uint32_t cp[CW_PH][MAX_BATCH + 1];      // units of phase p in the requested buckets before j
     uint32_t nreq;
 };
+
+using WideLds = WideLdsT<WTILE, WBINS>;
+using WideLdsBig = WideLdsT<11264, 4096>;
 static_assert(sizeof(WideLds) <= sizeof(FillLds), "the wide views fit the fill's LDS");
+static_assert(sizeof(WideLdsBig) <= 160 * 1024, "one lfin workgroup per CU");
 
 // canonical ordered key of a sum: -0 -> +0 (the reference's float compare ties them)
 __device__ __forceinline__ uint32_t okey(uint32_t b) {
@@ -218,7 +232,9 @@ __device__ __forceinline__ uint64_t ldc(const uint64_t *p) { return *p; }
 // not listed have smaller sums than every listed one of R.  One workgroup;
 // every pass over global data keeps WB loads per thread in flight (the list as
 // 16-byte loads), and lookups by candidate index go through an LDS sample.
-__device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
+template <class WL>
+__device__ __noinline__ LeadOut leader(WL &W, const LeadIn I) {
+    constexpr uint32_t WT = WL::WT, NBH = WL::NBH, NBL = 31u - __builtin_clz(NBH);
     LeadOut O;
     O.ok = false;
     O.P = 0;
@@ -326,7 +342,7 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
     // ---- 2. R = {key >= okS} by (key desc, rf32(start) asc): counting sort
     //      into bins of the key's distance below the maximum, then ranks
     //      inside each bin, one LDS tile of whole bins at a time ----
-    const uint32_t D = kmax - okS, shb = bitlen(D) > 13u ? bitlen(D) - 13u : 0u, nbin = (D >> shb) + 1u;
+    const uint32_t D = kmax - okS, shb = bitlen(D) > NBL ? bitlen(D) - NBL : 0u, nbin = (D >> shb) + 1u;
     for (uint32_t b = tid; b < nbin; b += FILL_WG) hist[b] = 0;
     if (tid == 0) { W.v[4] = 0; W.v[5] = 0; }
     __syncthreads();
@@ -341,11 +357,12 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
     nr = uni(W.v[4]);
     LEAD_SUB(0);
     if (STG_CREW_STAMPS && tid == 0) { I.dbg[6] = m; I.dbg[7] = nr; }
-    {   // exclusive scan of the bins (16 per thread), and the largest bin
-        uint32_t c[16], s = 0, mx = 0;
+    {   // exclusive scan of the bins (NBH / FILL_WG per thread), and the largest bin
+        constexpr uint32_t PB = NBH / FILL_WG;
+        uint32_t c[PB], s = 0, mx = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 16; ++u) {
-            const uint32_t b = 16u * tid + u;
+        for (uint32_t u = 0; u < PB; ++u) {
+            const uint32_t b = PB * tid + u;
             c[u] = b < nbin ? hist[b] : 0u;
             s += c[u];
             mx = max(mx, c[u]);
@@ -353,8 +370,8 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
         uint32_t tot;
         uint32_t a = blk_excl_scan<FNW_F>(s, W.sh, &tot);
 #pragma unroll
-        for (uint32_t u = 0; u < 16; ++u) {
-            const uint32_t b = 16u * tid + u;
+        for (uint32_t u = 0; u < PB; ++u) {
+            const uint32_t b = PB * tid + u;
             if (b < nbin) hist[b] = a;
             a += c[u];
         }
@@ -362,18 +379,18 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
         if ((tid & 63u) == 0) atomicMax(&W.v[5], mx);
         __syncthreads();
     }
-    if (W.v[5] > WTILE) { O.why = 3; return O; }
+    if (W.v[5] > WT) { O.why = 3; return O; }
     LEAD_SUB(1);
     // hist[b]: the start of bin b.  Tiles of whole bins: one pass over the
     // list (cached loads) places the tile's entries in LDS, where they are
     // ranked; only the ranked entries are stored (no load waits behind them).
     uint32_t tie_any = 0;
     for (uint32_t s0 = 0, b0 = 0; s0 < nr;) {
-        if (tid == 0) {  // the largest b1 <= nbin with start(b1) <= s0 + WTILE (start(nbin) = nr)
+        if (tid == 0) {  // the largest b1 <= nbin with start(b1) <= s0 + WT (start(nbin) = nr)
             uint32_t lo = b0 + 1u, hi = nbin;
             while (lo < hi) {
                 const uint32_t md = (lo + hi + 1u) >> 1;
-                if ((md < nbin ? hist[md] : nr) <= s0 + WTILE) lo = md; else hi = md - 1u;
+                if ((md < nbin ? hist[md] : nr) <= s0 + WT) lo = md; else hi = md - 1u;
             }
             W.v[6] = lo;
         }
@@ -457,7 +474,7 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
                         if (is_desc(cf + 1u, ce + 1u)) add_root(ce);
                     });
         // lookups by candidate index: the list is in candidate order; smp[j] = cx(j S)
-        const uint32_t S = (m + WTILE - 1u) / WTILE, ns = (m + S - 1u) / S;
+        const uint32_t S = (m + WT - 1u) / WT, ns = (m + S - 1u) / S;
         LEAD_SUB(3);
         uint32_t *const smp = W.u.s.ti;  // (past the replay's LDS)
         each_b<uint32_t>(ns, [&](uint32_t j) { return cx(j * S); }, [&](uint32_t j, uint32_t c) { smp[j] = c; });
@@ -492,7 +509,7 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
         //     the parent or sibling: the late lines listed first (in the
         //     replay's LDS, free here), then one lookup pair per thread
         uint32_t *const late = reinterpret_cast<uint32_t *>(W.u.sim);
-        constexpr uint32_t LATE_CAP = WTILE;
+        constexpr uint32_t LATE_CAP = WT;
         if (tid == 0) W.v[9] = 0;
         __syncthreads();
         each_b<uint64_t>(nr, [&](uint32_t rr) { return ldc(&gs[rr]); }, [&](uint32_t, uint64_t s) {
@@ -627,9 +644,9 @@ __device__ __noinline__ LeadOut leader(WideLds &W, const LeadIn I) {
             LEAD_SUB(5);
             // re-order every run by the replayed positions (rf32), one LDS tile
             // of whole runs at a time
-            uint32_t *const dd = W.u.s.hist, *const rfk = W.u.s.hist + WTILE, *const oo = W.u.s.ti;
+            uint32_t *const dd = reinterpret_cast<uint32_t *>(W.u.s.tk), *const rfk = dd + WT, *const oo = W.u.s.ti;
             for (uint32_t s0 = 0; s0 < nr;) {
-                const uint32_t nt = min(WTILE, nr - s0), ext = s0 + nt < nr ? 1u : 0u;
+                const uint32_t nt = min(WT, nr - s0), ext = s0 + nt < nr ? 1u : 0u;
                 each_b<uint2>(nt, [&](uint32_t j) { return make_uint2(ldc(&go[s0 + j]), ldc(&gs32[2u * (s0 + j) + 1u])); },
                               [&](uint32_t j, uint2 x) { oo[j] = x.x; dd[j] = x.y; });
                 if (tid == 0) W.v[11] = ext ? ldc(&gs32[2u * (s0 + nt) + 1u]) : NONE;
@@ -738,13 +755,13 @@ __device__ __forceinline__ CrewMap crew_map(const CrewBk &B) {
 }
 
 // A: one unit of la lines.
-template <uint32_t DA>
-__device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, uint32_t u) {
+template <uint32_t DA, class WL>
+__device__ __noinline__ void crew_a(WL &W, const CrewBk &B, CrewCtl *ctl, uint32_t u) {
     u = uni(u);  // (a callee's arguments arrive in VGPRs)
     ctl = uni_ptr(ctl);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6), q = lane & 3u;
     const CrewMap cm = crew_map(B);
-    uint32_t *const hist = W.u.s.hist;
+    uint32_t *const hist = W.u.hist8;
     for (uint32_t b = tid; b < WBINS; b += FILL_WG) hist[b] = 0;
     __syncthreads();
     const uint32_t nb = uni(B.d.nb);
@@ -797,7 +814,8 @@ __device__ __noinline__ void crew_a(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
 // C: the level-1 bin beta of the (sel + 1)-th largest candidate key (every
 // unit picks it from the bucket's histogram), then the candidates of bins >=
 // beta in keys [c * LC, ...), listed in scan order.
-__device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, uint32_t c, uint32_t epoch) {
+template <class WL>
+__device__ __noinline__ bool crew_c(WL &W, const CrewBk &B, CrewCtl *ctl, uint32_t c, uint32_t epoch) {
     c = uni(c);
     epoch = uni(epoch);
     ctl = uni_ptr(ctl);
@@ -811,7 +829,7 @@ __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
     for (uint32_t j = 0; j < 4; ++j) kv[j] = __builtin_amdgcn_raw_buffer_load_b128(rk, (K0 + 4u * j) * 4u, 0, 16 /* sc1 */);
     {   // the histogram into LDS beside them (8,192 words: 32 chunks of 64 lanes x 16 bytes)
         const char *const src = reinterpret_cast<const char *>(ctl->hist);
-        char *const dst = reinterpret_cast<char *>(W.u.s.hist);
+        char *const dst = reinterpret_cast<char *>(W.u.hist8);
         for (uint32_t ch = wave; ch < WBINS / 256u; ch += FNW_F)
             __builtin_amdgcn_global_load_lds(src + (size_t)(ch * 64u + lane) * 16u, dst + ch * 1024u, 16, 0, 16 /* sc1 */);
     }
@@ -824,7 +842,7 @@ __device__ __noinline__ bool crew_c(WideLds &W, const CrewBk &B, CrewCtl *ctl, u
         uint32_t hc[PER], s = 0;
 #pragma unroll
         for (uint32_t j = 0; j < PER; ++j) {
-            hc[j] = W.u.s.hist[WBINS - 1u - (PER * tid + j)];
+            hc[j] = W.u.hist8[WBINS - 1u - (PER * tid + j)];
             s += hc[j];
         }
         if (tid == 0) { W.v[0] = 0; W.v[1] = 0; }
@@ -923,8 +941,8 @@ __device__ __forceinline__ uint32_t phase_units(const CrewBk &B, uint32_t p) {
 
 // LONE: a one-bucket fill launch (one workgroup per CU, the kernel's register
 // budget is not shared with scans): phase A keeps twice the loads in flight
-template <bool LONE>
-__device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A) {
+template <bool LONE, class WL>
+__device__ __noinline__ void crew_loop(WL &W, FillLds &S, const CrewArgs A) {
     const uint32_t tid = threadIdx.x;
     CallCtl *const cc = A.cc;
     uint32_t *const ticket = &cc->crew_ticket[0], *const done = &cc->crew_done[0];  // zeroed for each call by the scan
@@ -1016,7 +1034,7 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
             const uint32_t *const lp = cm.lp;
             const uint32_t tpos = uni(B.d.nb) * 16u, nl1 = nL ? nL - 1u : 0u;
             const uint32_t per = (P + CW_NE - 1u) / CW_NE;
-            uint32_t *const posl = W.u.s.hist;  // WBINS words
+            uint32_t *const posl = W.u.hist8;  // WBINS words
             for (uint32_t i0 = rel * per, i1 = min(P, (rel + 1u) * per); i0 < i1; i0 += WBINS) {
                 const uint32_t ie = min(i1, i0 + WBINS);
                 each_b2<uint32_t, uint32_t>(ie - i0, [&](uint32_t j) { return ld_sc1(&go[i0 + j]) & LNONE; },
@@ -1036,7 +1054,8 @@ __device__ __noinline__ void crew_loop(WideLds &W, FillLds &S, const CrewArgs A)
 
 // Units and tickets of the requested buckets (W.bk[0 .. nreq) filled).
 // A's units: the bucket's lines over the crew (at least CW_LA lines each).
-__device__ __forceinline__ void crew_plan(WideLds &W, uint32_t ncrew) {
+template <class WL>
+__device__ __forceinline__ void crew_plan(WL &W, uint32_t ncrew) {
     if (threadIdx.x == 0) {
         uint32_t t = 0;
         for (uint32_t j = 0; j < W.nreq; ++j) {
@@ -1097,7 +1116,7 @@ __device__ __forceinline__ void crew_lfin(LfinLds &Lf, const Tv16FillArgs &A) {
         D.regimeB ? (TV16_DEC_B | (D.tail_cand ? TV16_DEC_TAIL : 0u) | (D.listw ? TV16_DEC_WIN : 0u)) : 0u;
     const bool want = crew_wants(flags, D.M, A.mode) && !ld_sc1(A.fail);
     __syncthreads();  // every read of the lfin view is done
-    WideLds &W = *reinterpret_cast<WideLds *>(&Lf);
+    WideLdsBig &W = *reinterpret_cast<WideLdsBig *>(&Lf);
     if (threadIdx.x == 0) {
         W.nreq = want ? 1u : 0u;
         if (want) {
