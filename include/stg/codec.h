@@ -127,6 +127,19 @@ int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
 int stg_merge_gather_compress_device(stg_codec_t h, const stg_bucket_t *bucket, float *d_residual,
                                      const float *const *d_grads, int num_gpus, void *stream);
 
+/* Batched compress_device whose emission writes the wire form of each stream
+ * (comm_manager.cpp:486-590 queueTx's packing, fused into the codec): bucket
+ * i's pairs land in d_idx / d_val as stg_wire_encode_device(flags[i]) would
+ * write them for the count = min(idx_cap, n) pairs the codec emits -- u16
+ * indices when flags[i] & STG_WIRE_U16_IDX, fp16 values when
+ * flags[i] & STG_WIRE_F16_VAL (the buffers hold count elements of that type),
+ * the codec's own u32 / f32 otherwise.  The same bytes as
+ * stg_codec_compress_batch_device followed by one encode per bucket, without
+ * the encode pass.  *d_count as in compress_device.  thresholdv16 only
+ * (STG_ERR_UNSUPPORTED for the other codecs).  Async on `stream`. */
+int stg_codec_compress_wire_batch_device(stg_codec_t h, const stg_bucket_t *buckets, const int *flags,
+                                         size_t nbuckets, void *stream);
+
 /* Per-key AIMD state (thresholdv16.cpp:243-259, thresholdv.cpp:72-80), read
  * back for parity tests; synchronises `stream`.  Returns STG_ERR_INVALID when
  * the key has never been compressed.  For threshold-v pass the src pointer

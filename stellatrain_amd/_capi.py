@@ -78,6 +78,8 @@ _SIGS = {
                                      C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.c_void_p]),
     "stg_adam_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "stg_merge_compress_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    "stg_codec_compress_wire_batch_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                                       C.c_void_p]),
     "stg_merge_gather_compress_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                                    C.c_void_p]),
     "stg_gather_slice": (C.c_int, [C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -102,7 +102,7 @@ class Compressor:
         if rc:
             check(rc)
 
-    def compress_batch_async(self, items, stream=None, counts=None, residuals=None):
+    def compress_batch_async(self, items, stream=None, counts=None, residuals=None, wire_flags=None):
         """Batched device compress (``stg_codec_compress_batch_device``): the
         same results as ``compress_async`` on each (name, src, k, dst_idx,
         dst_val[, idx_offset]) in order, on one stream.  Returns a
@@ -110,7 +110,11 @@ class Compressor:
         ``residuals`` (one float32 tensor per item) it is the MERGE compress
         with error feedback (``stg_merge_compress_batch_device``,
         compress.cpp:139-186): every src is zeroed at its dst_idx slots and its
-        residual receives the zeroed bucket."""
+        residual receives the zeroed bucket.  With ``wire_flags`` (one STG_WIRE_*
+        flag per item; thresholdv16) the emission writes each stream's wire form
+        (``stg_codec_compress_wire_batch_device``, comm_manager.cpp:486-590):
+        dst_idx is int16 under flag 1, dst_val float16-sized under flag 2, their
+        numel the pair capacity."""
         import torch
         if not items:
             return None
@@ -129,6 +133,12 @@ class Compressor:
             arr[j] = StgBucket(kb, src.data_ptr(), src.numel(), int(k), di.data_ptr(), di.numel(), dv.data_ptr(),
                                dv.numel(), int(off), counts.data_ptr() + 4 * j)
         sp = stream if stream is not None else _stream_ptr(dev.index)
+        if wire_flags is not None:
+            if residuals is not None or len(wire_flags) != len(items):
+                raise ValueError("wire_flags: one flag per bucket, no residuals")
+            fl = (C.c_int * len(items))(*[int(f) for f in wire_flags])
+            check(lib().stg_codec_compress_wire_batch_device(self._h, arr, fl, len(items), C.c_void_p(sp)))
+            return counts
         if residuals is None:
             check(lib().stg_codec_compress_batch_device(self._h, arr, len(items), C.c_void_p(sp)))
             return counts

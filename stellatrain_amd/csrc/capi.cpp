@@ -464,7 +464,7 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
 // share one launch; the per-key state makes a repeated key wait for the
 // launch that updates it.
 int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s, float *const *resid = nullptr,
-             const stg::GatherArgs *gather = nullptr) {
+             const stg::GatherArgs *gather = nullptr, const int *wire_flags = nullptr) {
     HIP_TRY(hipSetDevice(h->device));
     Workspace *ws = nullptr;
     int rc = h->workspace(s, &ws);
@@ -498,6 +498,7 @@ int run_tv16(stg_codec *h, const stg_bucket_t *bk, size_t nbk, hipStream_t s, fl
         t.first = fresh;
         t.resid = resid ? resid[i] : nullptr;
         t.gather = i == 0 ? gather : nullptr;
+        t.wflag = wire_flags ? (uint32_t)wire_flags[i] & 3u : 0u;
         grp.push_back(t);
     }
     return launch_tv16_group(h, ws, grp, s);
@@ -790,6 +791,23 @@ int stg_merge_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, 
     for (size_t i = 0; i < nbuckets; ++i)
         if (buckets[i].n && (rc = ef_after(h, buckets[i], d_residuals[i], fused, s))) return rc;
     return STG_OK;
+}
+
+int stg_codec_compress_wire_batch_device(stg_codec_t h, const stg_bucket_t *buckets, const int *flags,
+                                         size_t nbuckets, void *stream) {
+    CritPath crit_path;
+    if (!h) return fail(STG_ERR_INVALID, "null codec handle");
+    if (nbuckets && (!buckets || !flags)) return fail(STG_ERR_INVALID, "null bucket or flag array");
+    if (h->method != M_TV16)
+        return fail(STG_ERR_UNSUPPORTED, "wire-form emission is fused into thresholdv16 only "
+                                         "(compress, then stg_wire_encode_device)");
+    for (size_t i = 0; i < nbuckets; ++i) {
+        const stg_bucket_t &b = buckets[i];
+        const int rc = validate(h, b.n, b.k, b.idx_cap, b.val_cap, b.d_count);
+        if (rc) return rc;
+        if (flags[i] & ~3) return fail(STG_ERR_INVALID, "unknown wire flag bits");
+    }
+    return run_tv16(h, buckets, nbuckets, static_cast<hipStream_t>(stream), nullptr, nullptr, flags);
 }
 
 int stg_merge_gather_compress_device(stg_codec_t h, const stg_bucket_t *bucket, float *d_residual,

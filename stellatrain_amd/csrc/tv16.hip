@@ -145,7 +145,7 @@ __global__ void tv16_init_state(KeyState *st, const RSel *rs) {
 // ---------------------------------------------------------------------------
 // batched persistent kernel
 // ---------------------------------------------------------------------------
-struct BucketDesc {  // 80 bytes
+struct BucketDesc {  // 88 bytes
     const float *src;
     uint32_t *idx;
     float *val;
@@ -156,6 +156,7 @@ struct BucketDesc {  // 80 bytes
     int32_t idx_offset;
     uint32_t cs, nc;  // chunks [cs, cs + nc) of the launch's chunk sequence (nc >= 1)
     float *resid;     // fused error feedback: the streaming waves copy every full line here (or null)
+    uint32_t wflag, wend;  // wire form of the emitted pairs (wire_dev.h; 0: u32 / f32)
 };
 
 struct BatchArgs {
@@ -525,15 +526,13 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k) {
                 const float4 x = L.stage[par][e * 4 + q];
                 const uint32_t bi = pos + (uint32_t)d.idx_offset;
                 if (vec && len == 16) {
-                    *reinterpret_cast<float4 *>(d.val + off) = x;
-                    *reinterpret_cast<uint4 *>(d.idx + off) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                    put_pair4(d, off, bi, x);
                 } else {
                     const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                     for (uint32_t cc = 0; cc < 4; ++cc) {
                         if (4 * q + cc < len) {
-                            d.val[off + cc] = xs[cc];
-                            d.idx[off + cc] = bi + cc;
+                            put_pair(d, off + cc, bi + cc, xs[cc]);
                         }
                     }
                 }
@@ -627,8 +626,7 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k) {
             if (ct) {
                 const size_t p0 = (size_t)d.nb * 16;
                 for (uint32_t i = 0; i < ct; ++i) {
-                    d.val[c0 + i] = d.src[p0 + i];
-                    d.idx[c0 + i] = (uint32_t)(p0 + i) + (uint32_t)d.idx_offset;
+                    put_pair(d, c0 + i, (uint32_t)(p0 + i) + (uint32_t)d.idx_offset, d.src[p0 + i]);
                 }
             }
             d.state->t = regimeB ? (float)((double)t * 0.99) : t + inc;
@@ -794,6 +792,11 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         d.tl = (uint32_t)(b.n % 16);
         d.dst_len = b.dst_len;
         d.idx_offset = b.idx_offset;
+        {  // the wire stream is the count = min(dst_len, n) pairs written
+            const uint64_t numel = std::min<uint64_t>(b.dst_len, b.n);
+            d.wflag = b.wflag & 3u;
+            d.wend = numel ? (uint32_t)(8 * ((numel - 1) / 8)) : 0u;
+        }
         d.cs = K;
         d.nc = std::max<uint32_t>(1, (d.nb + TV16_CHUNK - 1) / TV16_CHUNK);
         K += d.nc;
@@ -806,6 +809,8 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         f.tl = d.tl;
         f.dst_len = d.dst_len;
         f.idx_offset = d.idx_offset;
+        f.wflag = d.wflag;
+        f.wend = d.wend;
         f.cand = ws.cand + (size_t)i * CAND_WORDS;
         f.heap = reinterpret_cast<uint2 *>(b.sums);
     }
@@ -885,7 +890,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.resid = a.b[0].resid;
         F.crew = crew_lone(a.num_cu, workers + rankers);
         F.crew_ctl = ws.crew;
-        if ((e = launch_tv16_fill(F, s)) != hipSuccess) return e;
+        if ((e = launch_tv16_fill_any(F, s)) != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[2], s);
         return hipGetLastError();
     }
@@ -921,7 +926,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.cc = &ws.ctl->cc[a.epoch & 1u];
         F.crew = F.lone ? crew_lone(a.num_cu, F.nbk + F.helpers) : crew_batch();
         F.crew_ctl = ws.crew;
-        const hipError_t e = launch_tv16_fill(F, s);
+        const hipError_t e = launch_tv16_fill_any(F, s);
         if (e != hipSuccess) return e;
     }
     if (a.ev) (void)hipEventRecord(a.ev[2], s);

@@ -5,6 +5,7 @@
 #include <algorithm>
 
 #include "ws.h"
+#include "wire_dev.h"
 
 namespace stg {
 namespace tv16 {
@@ -68,19 +69,15 @@ template <typename D>
 __device__ __forceinline__ void emit_line(const D &d, bool vec, uint32_t pos, uint32_t off, uint32_t len) {
     if (vec && len == 16) {
         const float4 *s4 = reinterpret_cast<const float4 *>(d.src + pos);
-        float4 *v4 = reinterpret_cast<float4 *>(d.val + off);
-        uint4 *i4 = reinterpret_cast<uint4 *>(d.idx + off);
         const uint32_t b = pos + (uint32_t)d.idx_offset;
         const float4 x0 = s4[0], x1 = s4[1], x2 = s4[2], x3 = s4[3];
-        v4[0] = x0; v4[1] = x1; v4[2] = x2; v4[3] = x3;
-        i4[0] = make_uint4(b + 0, b + 1, b + 2, b + 3);
-        i4[1] = make_uint4(b + 4, b + 5, b + 6, b + 7);
-        i4[2] = make_uint4(b + 8, b + 9, b + 10, b + 11);
-        i4[3] = make_uint4(b + 12, b + 13, b + 14, b + 15);
+        put_pair4(d, off, b, x0);
+        put_pair4(d, off + 4, b + 4, x1);
+        put_pair4(d, off + 8, b + 8, x2);
+        put_pair4(d, off + 12, b + 12, x3);
     } else {
         for (uint32_t i = 0; i < len; ++i) {
-            d.val[off + i] = d.src[(size_t)pos + i];
-            d.idx[off + i] = pos + i + (uint32_t)d.idx_offset;
+            put_pair(d, off + i, pos + i + (uint32_t)d.idx_offset, d.src[(size_t)pos + i]);
         }
     }
 }

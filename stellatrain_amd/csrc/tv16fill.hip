@@ -46,6 +46,14 @@
 // bucket of 2^20+ lines): the candidate vector is built in global memory and
 // make_heap / pop_heap run literally (make_heap level-parallel: subtrees of
 // one level are disjoint).  Slow (milliseconds at 64 MiB), exact, rare.
+//
+// Built twice (Makefile): tv16fill.o with STG_WIRE_EMIT=0 writes the codec's
+// u32 / f32 stream, with the registers of a fill that has no wire stores;
+// tv16fillw.o (STG_WIRE_EMIT=1) also writes the wire form (wire_dev.h) and is
+// launched when a bucket of the call asks for it.
+#ifndef STG_WIRE_EMIT
+#define STG_WIRE_EMIT 0
+#endif
 #include <algorithm>
 #include <cstddef>
 
@@ -209,9 +217,11 @@ __device__ __forceinline__ uint32_t rf_key(uint32_t pos) {
 // offset cnt + 16 i (less 16 - tl after the tail), at most rem elements.  Four
 // lanes per line (a float4 each: one 64-byte request per line), eight rounds
 // of loads in flight before their stores.
-template <uint32_t K = 5, typename GetPos>
-__device__ __forceinline__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np, uint32_t tail_rank,
-                           GetPos pos_of, uint32_t i_lo = 0, uint32_t i_hi = 0xffffffffu) {
+// W: the stream's wire form (one instance per form, so that the plain one's
+// registers are those of a kernel without the wire stores).
+template <uint32_t K, bool W, typename GetPos>
+__device__ __forceinline__ void emit_order_w(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np,
+                                             uint32_t tail_rank, GetPos pos_of, uint32_t i_lo, uint32_t i_hi) {
     np = min(np, i_hi);  // ranks [i_lo, min(np, i_hi)) of the order
     constexpr uint32_t LPR = FILL_WG / 4;  // lines per round; K rounds of loads in flight
     const bool vec = aligned16(d) && (cnt & 3u) == 0;
@@ -240,18 +250,22 @@ __device__ __forceinline__ void emit_order(const Tv16FillBucket &d, uint32_t cnt
             if (!len) continue;
             const uint32_t pos = pos_of(i), o = cnt + off + 4 * q, bi = pos + 4 * q + (uint32_t)d.idx_offset;
             if (vec && len == 16 && (off & 3u) == 0) {
-                *reinterpret_cast<float4 *>(d.val + o) = x[r];
-                *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                put_pair4_w<W>(d, o, bi, x[r]);
             } else {
                 for (uint32_t c = 0; c < 4; ++c) {
                     if (4 * q + c < len) {
-                        d.val[o + c] = d.src[(size_t)pos + 4 * q + c];
-                        d.idx[o + c] = bi + c;
+                        put_pair_w<W>(d, o + c, bi + c, d.src[(size_t)pos + 4 * q + c]);
                     }
                 }
             }
         }
     }
+}
+template <uint32_t K = 5, typename GetPos>
+__device__ __forceinline__ void emit_order(const Tv16FillBucket &d, uint32_t cnt, uint32_t rem, uint32_t np, uint32_t tail_rank,
+                           GetPos pos_of, uint32_t i_lo = 0, uint32_t i_hi = 0xffffffffu) {
+    if (STG_WIRE_EMIT && d.wflag) emit_order_w<K, true>(d, cnt, rem, np, tail_rank, pos_of, i_lo, i_hi);
+    else emit_order_w<K, false>(d, cnt, rem, np, tail_rank, pos_of, i_lo, i_hi);
 }
 
 // The orderer's emission of the pops' order: with helper workgroups (a lone
@@ -667,7 +681,7 @@ tv16_fill(Tv16FillArgs A) {
         const float *src = d.src;
         uint32_t *oidx = d.idx;
         float *oval = d.val;
-        const uint32_t tl = d.tl, ioff = (uint32_t)d.idx_offset;
+        const uint32_t tl = d.tl, ioff = (uint32_t)d.idx_offset, wflag = d.wflag, wend = d.wend;
         const bool vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(oidx) |
                            reinterpret_cast<uintptr_t>(oval)) & 15u) == 0 && (cnt & 3u) == 0;
         const uint32_t i1 = min(P, (share + 1) * chunk), q = tid & 3u;
@@ -677,13 +691,12 @@ tv16_fill(Tv16FillArgs A) {
             const uint32_t len = min(i == tail_rank ? tl : 16u, rem - o16);
             const uint32_t pos = ld_sc1(&order_g[i]), o = cnt + o16 + 4 * q, bi = pos + 4 * q + ioff;
             if (vec && len == 16 && (o16 & 3u) == 0) {
-                *reinterpret_cast<float4 *>(oval + o) = reinterpret_cast<const float4 *>(src + (size_t)pos)[q];
-                *reinterpret_cast<uint4 *>(oidx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+                wire_put4(oidx, oval, STG_WIRE_EMIT ? wflag : 0u, wend, o, bi,
+                          reinterpret_cast<const float4 *>(src + (size_t)pos)[q]);
             } else {
                 for (uint32_t c = 0; c < 4; ++c) {
                     if (4 * q + c < len) {
-                        oval[o + c] = src[(size_t)pos + 4 * q + c];
-                        oidx[o + c] = bi + c;
+                        wire_put(oidx, oval, STG_WIRE_EMIT ? wflag : 0u, wend, o + c, bi + c, src[(size_t)pos + 4 * q + c]);
                     }
                 }
             }
@@ -1257,7 +1270,11 @@ tv16_fill(Tv16FillArgs A) {
 constexpr size_t LFIN_LDS = std::max(std::max(sizeof(FillLds), sizeof(LfinLds)), sizeof(WideLdsBig));
 static_assert(LFIN_LDS <= 160 * 1024, "one lfin workgroup per CU");
 
+#if STG_WIRE_EMIT
+hipError_t launch_tv16_fill_wire(const Tv16FillArgs &a, hipStream_t s) {
+#else
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s) {
+#endif
     if (!a.nbk) return hipSuccess;
     static const hipError_t attr0 =
         hipFuncSetAttribute(reinterpret_cast<const void *>(&tv16_fill<false>), hipFuncAttributeMaxDynamicSharedMemorySize,

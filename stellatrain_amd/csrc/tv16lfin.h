@@ -221,15 +221,13 @@ __device__ __forceinline__ void lfin_store(const Tv16FillBucket &d, bool vec, ui
     const uint32_t len = g == kb ? r : 16u, off = 16 * g + 4 * q, pos = line * 16 + 4 * q;
     const uint32_t bi = pos + (uint32_t)d.idx_offset;
     if (vec && len == 16) {
-        *reinterpret_cast<float4 *>(d.val + off) = x;
-        *reinterpret_cast<uint4 *>(d.idx + off) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+        put_pair4(d, off, bi, x);
     } else {
         const float xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
         for (uint32_t cc = 0; cc < 4; ++cc)
             if (4 * q + cc < len) {
-                d.val[off + cc] = xs[cc];
-                d.idx[off + cc] = bi + cc;
+                put_pair(d, off + cc, bi + cc, xs[cc]);
             }
     }
 }
@@ -295,8 +293,7 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
         if (D.ct) {
             const size_t p0 = (size_t)d.nb * 16;
             for (uint32_t i = 0; i < D.ct; ++i) {
-                d.val[D.c0 + i] = d.src[p0 + i];
-                d.idx[D.c0 + i] = (uint32_t)(p0 + i) + (uint32_t)d.idx_offset;
+                put_pair(d, D.c0 + i, (uint32_t)(p0 + i) + (uint32_t)d.idx_offset, d.src[p0 + i]);
             }
         }
         if (A.resid && d.tl)  // fused error feedback: the ragged tail is not streamed
@@ -542,13 +539,11 @@ __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
         if (!len[u]) return;
         const uint32_t o = D.cnt + off[u] + 4 * q, bi = pos[u] + 4 * q + (uint32_t)d.idx_offset;
         if (vec && len[u] == 16 && (off[u] & 3u) == 0) {
-            *reinterpret_cast<float4 *>(d.val + o) = x;
-            *reinterpret_cast<uint4 *>(d.idx + o) = make_uint4(bi, bi + 1, bi + 2, bi + 3);
+            put_pair4(d, o, bi, x);
         } else {
             for (uint32_t cc = 0; cc < 4; ++cc)
                 if (4 * q + cc < len[u]) {
-                    d.val[o + cc] = d.src[(size_t)pos[u] + 4 * q + cc];
-                    d.idx[o + cc] = bi + cc;
+                    put_pair(d, o + cc, bi + cc, d.src[(size_t)pos[u] + 4 * q + cc]);
                 }
         }
     };

@@ -14,76 +14,30 @@
 // Both sides reproduce those bytes, so a stream packed here decodes on a
 // reference peer exactly as one packed by the reference, and vice versa.
 //
-// One element per lane, grid-stride: the stream is k pairs (1.3 MB at 64 MiB,
-// k = 1 %), so the launch is latency-bound; loads and stores are coalesced
+// The per-element casts live in wire_dev.h, shared with the thresholdv16
+// emission that writes the wire form directly.  One element per lane,
+// grid-stride: the stream is k pairs (1.3 MB at 64 MiB, k = 1 %), so the launch is latency-bound; loads and stores are coalesced
 // 4-byte / 2-byte runs per wave.  The fp16 conversion is integer arithmetic so
 // NaN payloads and subnormals match the x86 instruction bit for bit.
 #include <algorithm>
 
 #include "ws.h"
+#include "wire_dev.h"
 
 namespace stg {
 
 namespace {
-
-__device__ __forceinline__ uint32_t f32_to_f16_rne(uint32_t u) {
-    const uint32_t sign = (u >> 16) & 0x8000u;
-    const uint32_t ex = (u >> 23) & 0xffu;
-    uint32_t man = u & 0x7fffffu;
-    if (ex == 0xffu) return sign | 0x7c00u | (man ? 0x200u | (man >> 13) : 0u);
-    const int e = (int)ex - 112;
-    if (e >= 31) return sign | 0x7c00u;
-    if (e <= 0) {
-        if (e < -10) return sign;
-        man |= 0x800000u;
-        const uint32_t shift = (uint32_t)(14 - e);
-        uint32_t h = man >> shift;
-        const uint32_t rem = man & ((1u << shift) - 1u), half = 1u << (shift - 1);
-        if (rem > half || (rem == half && (h & 1u))) ++h;
-        return sign | h;
-    }
-    uint32_t h = ((uint32_t)e << 10) | (man >> 13);
-    const uint32_t rem = man & 0x1fffu;
-    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
-    return sign | h;
-}
-
-__device__ __forceinline__ uint32_t f16_to_f32(uint32_t h) {
-    const uint32_t sign = (h & 0x8000u) << 16;
-    const uint32_t ex = (h >> 10) & 0x1fu;
-    uint32_t man = h & 0x3ffu;
-    if (ex == 0x1fu) return sign | 0x7f800000u | (man << 13);
-    if (ex) return sign | ((ex + 112u) << 23) | (man << 13);
-    if (!man) return sign;
-    const uint32_t lz = __clz(man) - 21;  // leading zeros within the 11-bit field (man < 0x400)
-    man <<= lz;
-    return sign | ((113u - lz) << 23) | ((man & 0x3ffu) << 13);
-}
-
-__device__ __forceinline__ uint32_t f32_to_u16_trunc(float f) {
-    int32_t t = INT32_MIN;  // vcvttss2si r32: invalid -> 0x80000000
-    if (f == f && f > -2147483904.0f && f < 2147483648.0f) t = (int32_t)f;
-    return (uint32_t)t & 0xffffu;
-}
 
 // one element of the encode (shared by the single and the batched launch)
 __device__ __forceinline__ void encode_one(const uint32_t *__restrict__ idx, const float *__restrict__ val, size_t i,
                                            size_t simd_end, uint32_t flag, void *__restrict__ idx_out,
                                            void *__restrict__ val_out) {
     const uint32_t x = idx[i];
-    if (flag & 1u) {
-        const int32_t v = (int32_t)x;
-        const uint32_t w = i < simd_end ? (uint32_t)(uint16_t)(int16_t)min(max(v, -32768), 32767) : (x & 0xffffu);
-        static_cast<uint16_t *>(idx_out)[i] = (uint16_t)w;
-    } else {
-        static_cast<uint32_t *>(idx_out)[i] = x;
-    }
+    if (flag & 1u) static_cast<uint16_t *>(idx_out)[i] = (uint16_t)wire_idx16(x, i, simd_end);
+    else static_cast<uint32_t *>(idx_out)[i] = x;
     const float f = val[i];
-    if (flag & 2u)
-        static_cast<uint16_t *>(val_out)[i] =
-            (uint16_t)(i < simd_end ? f32_to_f16_rne(__float_as_uint(f)) : f32_to_u16_trunc(f));
-    else
-        static_cast<float *>(val_out)[i] = f;
+    if (flag & 2u) static_cast<uint16_t *>(val_out)[i] = (uint16_t)wire_val16(f, i, simd_end);
+    else static_cast<float *>(val_out)[i] = f;
 }
 
 // Batched encode: the launch's workgroups are dealt to the buckets by the

@@ -183,6 +183,7 @@ struct Tv16Bucket {
                        // (2 words per line: (nb + 1) * 2 floats)
     float *resid;      // MERGE error feedback: receives the bucket's full lines, or null
     const GatherArgs *gather;  // intra-node gather-add fused into the scan (dst = src), or null
+    uint32_t wflag;    // the emission writes the wire form (STG_WIRE_* flags; idx / val typed by it)
 };
 struct Tv16Launch {
     const Tv16Bucket *b;
@@ -206,6 +207,7 @@ struct Tv16FillBucket {
     int32_t idx_offset;
     const uint32_t *cand;  // the bucket's window entries (CAND_WORDS)
     uint2 *heap;           // full-path scratch: (nb + 1) candidates {key bits, element position}
+    uint32_t wflag, wend;  // wire form of the emitted pairs (wire_dev.h; 0: u32 / f32)
 };
 struct Tv16FillArgs {
     Tv16FillBucket bk[MAX_BATCH];
@@ -240,6 +242,13 @@ struct Tv16FillArgs {
     float *resid;          // fused error feedback: the ragged tail is copied by the finish
 };
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
+// the same fill built to write the wire form of buckets with wflag set (tv16fill.hip)
+hipError_t launch_tv16_fill_wire(const Tv16FillArgs &a, hipStream_t s);
+inline hipError_t launch_tv16_fill_any(const Tv16FillArgs &a, hipStream_t s) {
+    bool w = false;
+    for (uint32_t i = 0; i < a.nbk; ++i) w |= a.bk[i].wflag != 0;
+    return w ? launch_tv16_fill_wire(a, s) : launch_tv16_fill(a, s);
+}
 // one-bucket scan (tv16lone.hip): every workgroup streams its chunks and lists
 // them; nothing waits on another workgroup
 struct LScanArgs {

@@ -517,6 +517,45 @@ def gather_fused(torch, calls):
     return out
 
 
+def wire_fused(torch, calls):
+    """The compressed stream's wire form (comm_manager.cpp:486-590; SURVEY 8f
+    row 3) written by the thresholdv16 emission
+    (stg_codec_compress_wire_batch_device) against compress then
+    stg_wire_encode_device: a 60,000-float bucket with u16 indices (queueTx's
+    flag for numel < 65536) and a 64 MiB bucket with fp16 values
+    (FP16_COMPRESSION).  Inputs rotate over >= 512 MB of device-resident
+    buckets, one key."""
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel, wire_encode
+    from stellatrain_amd._capi import lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    out = []
+    for n, flag in ((60000, 1), (16 << 20, 2)):
+        k = merge_numel(n, 0.99)
+        nbuf = max(2, math.ceil(512 / (n * 4 / (1 << 20))) + 1) if n >= (1 << 20) else 16
+        bufs = bufs_for(torch, lib(), dev, n, nbuf, st.cuda_stream, 820)
+        idx = torch.zeros(k, dtype=torch.int32, device=dev)
+        val = torch.zeros(k, dtype=torch.float32, device=dev)
+        wi = torch.zeros(k, dtype=torch.int16 if flag & 1 else torch.int32, device=dev)
+        wv = torch.zeros(k, dtype=torch.int16 if flag & 2 else torch.float32, device=dev)
+        counts = torch.zeros(1, dtype=torch.int32, device=dev)
+        row = {"config": f"thresholdv16 {n * 4 / (1 << 20):.2f} MiB k={k}, wire flag {flag}", "buffers": nbuf}
+        for fused in (True, False):
+            comp = ThresholdvCompressor16()
+
+            def step(s):
+                b = bufs[s % nbuf]
+                if fused:
+                    comp.compress_batch_async([("wf@w", b, k, wi, wv)], counts=counts, wire_flags=[flag])
+                else:
+                    comp.compress_batch_async([("wf@w", b, k, idx, val)], counts=counts)
+                    wire_encode(idx, val, flag, wi, wv)
+            row["fused_us" if fused else "separate_us"] = round(_time_loop(torch, st, step, calls, 8), 2)
+        out.append(row)
+        del bufs
+    return out
+
+
 def cpu_codec(method, mib, ratio, seconds):
     """The reference CPU path beside its GPU row, same run, this host's cores
     (north_star): oracle/_ref/libstg_ref.so (the reference's compress/*.cpp
@@ -587,7 +626,7 @@ def main():
     p.add_argument("--calls", type=int, default=48)
     p.add_argument("--c4-streams", type=int, default=4)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="per CPU baseline row (0: none)")
-    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,merge,ef,gather,gfused")
+    p.add_argument("--only", default="c2,c3,c4,c5,single,e2e,apply,merge,ef,gather,gfused,wfused")
     a = p.parse_args()
     import torch
     from stellatrain_amd import make_compressor
@@ -616,6 +655,9 @@ def main():
             emit(c5_round_trip(torch, a.calls, kind))
     if "gfused" in only:
         for r in gather_fused(torch, a.calls):
+            emit(r)
+    if "wfused" in only:
+        for r in wire_fused(torch, a.calls):
             emit(r)
     if "gather" in only:
         for d in gather(torch, a.calls):

@@ -93,6 +93,8 @@ for s in "$@"; do
         apply) step apply 300 python tools/bench_configs.py --only c5,apply ;;
         ef) step ef 300 python tools/bench_configs.py --only ef ;;
         gather) step gather 300 python tools/bench_configs.py --only gather ;;
+        wfused) step wfused 300 python tools/bench_configs.py --only wfused ;;
+        tests_wire) step tests_wire 600 python -u -m pytest tests/test_gpu_wire_fused.py tests/test_gpu_wire.py -v -m gpu --timeout 120 --timeout-method thread ;;
         prof_apply) step prof_apply 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_apply" -o run \
                 -- python3 tools/bench_configs.py --only apply ;;
         depths)  # tuning variants built as stellatrain_amd/libstg_codec_d*.so
