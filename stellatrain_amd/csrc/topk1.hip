@@ -276,6 +276,15 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
     const bool hit = ok && !ovf && th <= r && r - th < tband;
     if (!__syncthreads_or((int)hit)) return false;  // (uniform)
     const uint32_t rr = r - th;
+    // the emission unit's tile counts and offsets (emit_unit), loaded beside
+    // the fine bins: the ticket (L.v[9], taken before the pick) is back by now
+    const uint32_t u = L.v[9], t0 = u * A.ut;
+    const bool pre = t0 < A.nt && tid < std::min(A.ut, A.nt - t0);
+    uint32_t pc = 0, po = 0;
+    if (pre) {
+        pc = A.sup_n[t0 + tid];
+        po = A.sup_off[t0 + tid];
+    }
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
         if (above <= rr && rr < above + c[j]) { L.v[2] = TK2_COARSE - 1u - (PER * tid + j); L.v[3] = rr - above; }
@@ -285,6 +294,10 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
     const uint32_t cb = L.v[2], rc = L.v[3];
     const uint32_t f = A.fine[(cb << TK2_CSH) + (1u << TK2_CSH) - 1u - tid];  // top-down
     static_assert((1u << TK2_CSH) == STG_WG, "one fine bin per thread");
+    if (pre) {  // (after the fine load is issued: its round trip overlaps theirs)
+        L.uc[tid] = pc;
+        L.uo[tid] = po;
+    }
     if (tid == 0) L.v[4] = 0xffffffffu;
     uint32_t tot;
     const uint32_t fa = blk_excl_scan<STG_WAVES>(f, L.sh, &tot);
@@ -301,15 +314,19 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
 // their supersets, publishes them, sums the earlier units' (look-back: units
 // are taken in ticket order, so each is held by a running or finished
 // workgroup) and writes the winners at their offsets.  Returns false when a
-// wait gave up.
-__device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, uint32_t T, uint64_t need_eq) {
+// wait gave up.  `pre`: the tiles' counts and offsets are in L.uc / L.uo
+// already (pick_exact loads them).
+__device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, uint32_t T, uint64_t need_eq,
+                                       bool pre) {
     const uint32_t tid = threadIdx.x, nt = A.nt;
     const uint32_t UT = A.ut, t0 = u * UT, nT = std::min(UT, nt - t0);
-    if (tid < nT) {
-        L.uc[tid] = A.sup_n[t0 + tid];
-        L.uo[tid] = A.sup_off[t0 + tid];
+    if (!pre) {
+        if (tid < nT) {
+            L.uc[tid] = A.sup_n[t0 + tid];
+            L.uo[tid] = A.sup_off[t0 + tid];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (tid < 64) {  // the tiles' flat starts: one wave scans the counts
         const uint32_t c = tid < nT ? L.uc[tid] : 0u, o = tid < nT ? L.uo[tid] : 0u;
         const uint32_t incl = wave_incl_scan(c), ex = incl - c;
@@ -623,7 +640,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         __syncthreads();
         if (u < NU) {
             TK1_STAMP_MAX(48);  // the last unit taken
-            if (!emit_unit(A, L, u, P.T, need_eq)) { poison(); zero_next(); return; }
+            if (!emit_unit(A, L, u, P.T, need_eq, true)) { poison(); zero_next(); return; }
             TK1_STAMP_MAX(44);  // the last unit done
         }
         TK1_STAMP_MAX(45);      // the last workgroup out
@@ -786,9 +803,12 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     A.tile_gt = ws.tile_cnt;
     A.tile_eq = ws.tile_aux;
     A.fine = fine;
-    // a unit's superset (~ k / nt entries per tile) in about one round of ER per thread
+    // a unit's superset (~ k / nt entries per tile): about `per_unit` entries,
+    // so that the units spread over the CUs (STG_TK1_UNIT: entries per unit)
+    static const uint64_t per_unit =
+        getenv("STG_TK1_UNIT") ? (uint64_t)std::max(64, atoi(getenv("STG_TK1_UNIT"))) : (uint64_t)ER * STG_WG * 3 / 4;
     A.ut = (uint32_t)std::max<uint64_t>((nt + TK2_UNITS - 1) / TK2_UNITS,
-                                        std::min<uint64_t>(TK2_UT, (uint64_t)ER * STG_WG * nt / std::max<uint64_t>(A.k, 1)));
+                                        std::min<uint64_t>(TK2_UT, per_unit * nt / std::max<uint64_t>(A.k, 1)));
     A.ut = std::max(1u, std::min(A.ut, TK2_UT));
     A.fine_next = ws.tkfine + (size_t)((tag + 1u) & 1u) * TK2_FINE;
     A.dbg = ws.misc;
