@@ -572,7 +572,9 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         // superset entries (two words each, stg::TOPK_SUP_CAP per tile); per-tile
         // counts, their prefixes and the superset counts
         // + the level-2 bin's list (two words per key)
-        if ((rc = ws->ensure(2 * ntiles * stg::TOPK_SUP_CAP + 2 * stg::TOPK_LIST_CAP, 3 * ntiles + 1, 1))) return rc;
+        // (whole groups of TK2_REG tiles: topk1.hip's fixed superset slots)
+        const size_t stiles = (ntiles + stg::TK2_REG - 1) / stg::TK2_REG * stg::TK2_REG;
+        if ((rc = ws->ensure(2 * stiles * stg::TOPK_SUP_CAP + 2 * stg::TOPK_LIST_CAP, 3 * ntiles + 1, 1))) return rc;
         stg::TopkLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, h->method == M_TOPK, d_count,
                           h->num_cu, ev};
         const size_t m = h->method == M_TOPK ? (n + 3) / 4 : n;
