@@ -119,7 +119,10 @@ constexpr uint32_t TK2_CSH = 8;                       // coarse bins: 256 ulps
 constexpr uint32_t TK2_COARSE = TK2_FINE >> TK2_CSH;  // 1024
 constexpr uint32_t TK2_HI = 16;                       // shards of the count of keys above the band
 constexpr uint32_t TK2_REG = 32;                      // superset regions (tile mod 32), an offset counter each
-constexpr uint32_t TK2_UT = 16;                       // tiles per emission unit
+#ifndef STG_TK2_UT
+#define STG_TK2_UT 16
+#endif
+constexpr uint32_t TK2_UT = STG_TK2_UT;               // tiles per emission unit (at most)
 constexpr uint32_t TK2_UNITS = TOPK_LIST_TILES / TK2_UT;
 struct alignas(128) TopkCtl {
     uint32_t tk[TK1_NPH][TK1_SH][TK1_LINE];    // tickets per phase and shard
