@@ -583,8 +583,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
             KeyState *st;
             bool fresh;
             if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
-            if (++ws->tk_tag == 0) ws->tk_tag = 1;
-            HIP_TRY(stg::launch_topk1(a, ws->d, st, !fresh, ws->tk_tag, s));
+            HIP_TRY(stg::launch_topk1(a, ws->d, st, !fresh, &ws->tk_tag, s));
         } else {
             HIP_TRY(stg::launch_topk(a, ws->d, s));
         }

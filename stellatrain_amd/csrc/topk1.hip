@@ -651,9 +651,6 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         zero_next();
         return;
     }
-    if (blockIdx.x == 0 && tid == 0 && ld_sc1(&C->band_ok)) {  // a hinted call missed: widen the band
-        A.state->inc = fminf(2.0f * A.state->inc, D_MAX);
-    }
     // wait for the single-unit phase p's flag (one lane polls, sparsely)
     auto wait_flag = [&](uint32_t p) -> bool {
         if (tid == 0) {
@@ -685,7 +682,16 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
                 st_sc1(&C->res_T, T);
                 atomicAdd(&A.dbg[39], 1u);
                 A.state->t = u2f(T);
-                if (!A.state->init) A.state->inc = D_SEED;
+                if (!A.state->init) {
+                    A.state->inc = D_SEED;
+                } else if (ld_sc1(&C->band_ok)) {
+                    // a hinted call missed.  T outside [F, H): widen the band.
+                    // T inside it, but a superset overflowed its slots
+                    // (magnitudes dense near F): narrow it, since a wider band
+                    // would only admit more entries next call
+                    const bool in = ld_sc1(&C->band_F) <= T && T < ld_sc1(&C->band_H);
+                    A.state->inc = in ? fmaxf(0.5f * A.state->inc, D_MIN) : fminf(2.0f * A.state->inc, D_MAX);
+                }
                 A.state->init = 1;
             }
         } else if (p == M_CNT) {
@@ -751,9 +757,11 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
 
 }  // namespace
 
-hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, bool hinted, uint32_t tag,
+hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, bool hinted, uint32_t *tagp,
                         hipStream_t s) {
-    if (a.k == 0 || a.n == 0 || !tag) return hipErrorInvalidValue;
+    // k == 0 (topk.cpp accepts it: nothing selected, returns cap) takes the
+    // select's launcher, which writes the count alone; no hint is seeded
+    if (a.k == 0 || a.n == 0) return launch_topk(a, ws, s);
     uint64_t m = a.n, zeros = 0;
     uint32_t last_mask = 0xffffffffu;
     if (a.bug_compat) {  // memcpy(clone, src, n) copies n bytes (topk.cpp:31)
@@ -769,6 +777,18 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
         tk2_seed<<<1, 1, 0, s>>>(state, ws.rsel, ws.misc);
         return hipGetLastError();
     }
+    // The control block and band histogram alternate by the tag's parity: each
+    // tk_one zeroes the other parity's copies for the next hinted call.  So the
+    // tag moves only here, where tk_one runs, and always to the other parity
+    // (0 is never a tag: 0xffffffff is followed by 2).  A launch error leaves
+    // both copies in an unknown state; they are zeroed on the stream.
+    const uint32_t tag = *tagp + 1u == 0u ? 2u : *tagp + 1u;
+    *tagp = tag;
+    auto reset_ctl = [&](hipError_t e) {
+        (void)hipMemsetAsync(ws.tkctl, 0, 2 * sizeof(TopkCtl), s);
+        (void)hipMemsetAsync(ws.tkfine, 0, 2 * (size_t)TK2_FINE * sizeof(uint32_t), s);
+        return e;
+    };
     TopkCtl *const ctl = ws.tkctl + (tag & 1u);
     uint32_t *const fine = ws.tkfine + (size_t)(tag & 1u) * TK2_FINE;
     // superset regions: the bucket's share of TOPK_SUP_CAP entries per tile, in TK2_REG regions
@@ -830,7 +850,8 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     if (vec) tk_one<true><<<G, STG_WG, 0, s>>>(A);
     else tk_one<false><<<G, STG_WG, 0, s>>>(A);
     if (a.ev) (void)hipEventRecord(a.ev[2], s);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? e : reset_ctl(e);
 }
 
 }  // namespace stg

@@ -313,7 +313,7 @@ hipError_t launch_topk(const TopkLaunch &a, const DevWS &ws, hipStream_t s);
 // most TOPK_LIST_TILES tiles: a key's first call (!hinted) runs launch_topk and
 // seeds the hint; later calls stream once and emit (the select's way inside
 // the emission launch when the band misses)
-hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, bool hinted, uint32_t tag,
+hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, bool hinted, uint32_t *tag,
                         hipStream_t s);
 
 // Radix select: the key of descending rank `rank` among (bits(a[i]) & 0x7fffffff),

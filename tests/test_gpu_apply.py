@@ -76,6 +76,29 @@ def test_scatter_merge_parity(gpu, oracle, n, per_rank, world, overlap):
     scatter_merge_check()  # no device failure on this stream's scratch
 
 
+@pytest.mark.parametrize("case", __import__("merge_golden").MANIFEST_MERGE["merge"], ids=lambda c: c["name"])
+def test_scatter_merge_torch_goldens(gpu, case):
+    """The HIP MERGE decompress against torch's own CPU kernels running
+    cpu_optimize.cpp:40-72 (tests/golden/make_golden_merge.py): world 1-8,
+    shared and disjoint indices, -0.0 values, a rank stream with repeated
+    indices, and C5's 64 MiB bucket at world 2/4/8."""
+    import torch
+    from merge_golden import merge_case_check, merge_case_inputs
+    from stellatrain_amd import scatter_merge
+    from stellatrain_amd.engine import scatter_merge_check
+    idx, val = merge_case_inputs(case)
+    n = case["n"]
+    dense = torch.zeros(n, dtype=torch.float32, device=gpu)
+    mark = torch.zeros(n, dtype=torch.uint8, device=gpu)
+    out_i, out_v, cnt = scatter_merge(torch.from_numpy(idx.view(np.int32)).to(gpu), torch.from_numpy(val).to(gpu),
+                                      case["per_rank"], case["world"], n, dense=dense, mark=mark)
+    m = int(cnt.item())
+    merge_case_check(case, out_i[:m].cpu().numpy(), out_v[:m].cpu().numpy())
+    assert int(torch.count_nonzero(dense).item()) == 0
+    assert int(torch.count_nonzero(mark).item()) == 0
+    scatter_merge_check()
+
+
 def test_scatter_merge_world1_duplicates(gpu, oracle):
     """World 1 takes a copy path when no index repeats and the election path
     when one does (csrc/apply.hip win_mark's duplicate flag): alternate

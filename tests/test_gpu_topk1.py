@@ -97,3 +97,48 @@ def test_c2_steady_64mib(gpu, oracle):
         comp.check_device()
         w = _words(comp)
         assert w[38] >= 3 and w[39] == 1, w[36:40]
+
+
+@pytest.mark.parametrize("bug_compat", [False, True])
+def test_interleaved_keys(gpu, oracle, bug_compat):
+    """Keys appearing between hinted calls on one workspace: A, B, A, C, B, C,
+    D, A, ...  A key's first call runs the select's launches (no emission
+    launch), so the control block's call parity must move only with hinted
+    calls; every call against the oracle."""
+    from stellatrain_amd import TopkCompressor
+    comp = TopkCompressor(exact=not bug_compat)
+    n, k = (1 << 20) + 5, 10485
+    order = ["A", "B", "A", "C", "B", "C", "D", "A", "E", "B", "D", "E", "A", "F", "A"]
+    calls = {}
+    for key in order:
+        c = calls.get(key, 0)
+        calls[key] = c + 1
+        src = synth(n, seed_for(330 + ord(key), c), D1)
+        _check(gpu, oracle, comp, key, src, k, bug_compat)
+    comp.check_device()
+    w = _words(comp)
+    # every first call takes the select's way; hinted calls mostly hit (at
+    # this size a fresh bucket's k-th magnitude can land outside the band)
+    assert w[39] >= len(calls) and w[38] >= len(order) - 2 * len(calls), w[36:40]
+
+
+@pytest.mark.parametrize("bug_compat", [False, True])
+def test_k_zero(gpu, oracle, bug_compat):
+    """k = 0 on a bucket the one-pass path covers (topk.cpp accepts it: the
+    count is the capacity, nothing written), first and hinted calls, and a
+    hinted call after it still exact."""
+    import torch
+    from stellatrain_amd import TopkCompressor
+    comp = TopkCompressor(exact=not bug_compat)
+    n, k = 1 << 20, 10485
+    src = synth(n, seed_for(340, 0), D1)
+    _check(gpu, oracle, comp, "z", src, k, bug_compat)
+    for key in ("z", "fresh"):
+        idx = torch.zeros(4, dtype=torch.int32, device=gpu)
+        val = torch.zeros(4, dtype=torch.float32, device=gpu)
+        d = torch.from_numpy(src).to(gpu)
+        assert comp.compress(key, d, 0, idx, val, 0) == 4  # count = dst_idx.second (topk.cpp:25)
+        assert not idx.any() and not val.any()
+    _check(gpu, oracle, comp, "z", synth(n, seed_for(340, 1), D1), k, bug_compat)
+    _check(gpu, oracle, comp, "fresh", synth(n, seed_for(340, 2), D1), k, bug_compat)
+    comp.check_device()

@@ -153,3 +153,16 @@ def test_gather_slices_partition(oracle):
                 assert a == cur and b >= a
                 cur = b
             assert cur == n
+
+
+
+# MERGE decompress at world >= 1 pinned to torch's own CPU kernels
+# (tests/golden/make_golden_merge.py runs cpu_optimize.cpp:40-72's op sequence)
+from merge_golden import MANIFEST_MERGE, merge_case_check, merge_case_inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("case", MANIFEST_MERGE["merge"], ids=lambda c: c["name"])
+def test_merge_oracle_matches_torch(oracle, case):
+    idx, val = merge_case_inputs(case)
+    oi, ov = oracle.merge_decompress(idx, val, case["per_rank"], case["world"], case["n"])
+    merge_case_check(case, oi, ov)

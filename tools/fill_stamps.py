@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase timing of tv16_fill (workgroup 0) from s_memrealtime stamps.
 
-Needs the stamp build: make -C stellatrain_amd/csrc OUT=../libstg_codec_stamps.so
+Needs the stamp build: make -C stellatrain_amd/csrc OUT=../../tools/variants/libstg_codec_stamps.so
 BUILD=build_stamps EXTRA=-DSTG_FILL_STAMPS=1, selected with STG_CODEC_LIB.
 Prints, per call, the phase durations in microseconds (100 MHz clock)."""
 import ctypes as C

@@ -61,8 +61,8 @@ for s in "$@"; do
             python3 tools/ktrace.py gpurun_out/prof_merge 16 > gpurun_out/prof_merge.txt 2>&1 ;;
         scale_drop) step scale_drop 280 python tools/scale_drop.py 4 ${DROPS:-100,10,2,1.1} ;;
         fill_paths) step fill_paths 200 python tools/fill_paths.py --steps 400 ;;
-        stamps_r4) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_tk1st.so step tk1_stamps 150 python tools/tk1_stamps.py
-            STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_crewst.so step crew_stamps 150 python tools/crew_stamps.py ;;
+        stamps_r4) STG_CODEC_LIB=$R/tools/variants/libstg_codec_tk1st.so step tk1_stamps 150 python tools/tk1_stamps.py
+            STG_CODEC_LIB=$R/tools/variants/libstg_codec_crewst.so step crew_stamps 150 python tools/crew_stamps.py ;;
         tiny) step tiny 120 python tools/tiny_probe.py
             STG_TV16_CREW_LONE=0 step tiny_nocrew 120 python tools/tiny_probe.py
             STG_DEBUG_TV16_FILL=2 step tiny_literal 120 python tools/tiny_probe.py ;;
@@ -71,7 +71,7 @@ for s in "$@"; do
         c2ab)  # shipped-mode top-k: the ordered six-launch path (STG_TOPK_BK=0) against the unordered three
             STG_TOPK_BK=0 step c2_ordered 150 python tools/bench_configs.py --only topk --cpu-seconds 0
             step c2_bk 150 python tools/bench_configs.py --only topk --cpu-seconds 0
-            for L in stellatrain_amd/libstg_codec_bk*.so; do
+            for L in tools/variants/libstg_codec_bk*.so; do
                 [ -e "$L" ] || continue
                 v=$(basename $L .so); v=${v#libstg_codec_}
                 STG_CODEC_LIB=$R/$L step c2_$v 150 python tools/bench_configs.py --only topk --cpu-seconds 0
@@ -81,12 +81,12 @@ for s in "$@"; do
             python3 tools/ktrace.py gpurun_out/prof_c2 > gpurun_out/prof_c2.txt 2>&1 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
         tvvar)  # threshold-v variants built by tools/tv_variants.sh: C3 device timing each
-            for L in stellatrain_amd/libstg_codec_tv*.so; do
+            for L in tools/variants/libstg_codec_tv*.so; do
                 v=$(basename $L .so); v=${v#libstg_codec_}
                 STG_CODEC_LIB=$R/$L step c3_$v 150 python tools/bench_configs.py --only c3dev --calls 64
                 [ -n "${TV_TESTS:-}" ] && STG_CODEC_LIB=$R/$L step tests_tv_$v 300 python -u -m pytest tests/test_gpu_codecs.py -k "thresholdv_parity" -x -q -m gpu --timeout 120 --timeout-method thread
             done ;;
-        tv_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_tvst.so step tv_stamps 150 python tools/tv_stamps.py ;;
+        tv_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_tvst.so step tv_stamps 150 python tools/tv_stamps.py ;;
         tests_tv) step tests_tv 400 python -u -m pytest tests -k "thresholdv and not thresholdv16 or c3 or tv_" -v -m gpu --timeout 120 --timeout-method thread ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
         c5) step c5 300 python tools/bench_configs.py --only c5 ;;
@@ -98,7 +98,7 @@ for s in "$@"; do
         prof_apply) step prof_apply 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_apply" -o run \
                 -- python3 tools/bench_configs.py --only apply ;;
         depths)  # tuning variants built as stellatrain_amd/libstg_codec_d*.so
-            for L in stellatrain_amd/libstg_codec_*.so; do
+            for L in tools/variants/libstg_codec_*.so; do
                 v=$(basename $L .so); v=${v#libstg_codec_}
                 export STG_CODEC_LIB=$R/$L
                 step depth_$v 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-}
@@ -122,9 +122,9 @@ for s in "$@"; do
             step prof_lone 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_lone" -o run -- ./tools/lone_bench 0 96
             python3 tools/ktrace.py gpurun_out/prof_lone 12 > gpurun_out/prof_lone.txt 2>&1 ;;
         lfin_probe) step lfin_probe 200 python tools/lfin_probe.py ;;
-        prof_lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step prof_lfin_stamps 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lfin_stamps" -o run -- python3 tools/lfin_probe.py ;;
-        lfin_stamps) STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so step lfin_stamps 200 python tools/lfin_probe.py ;;
-        fill_stamps) FS_BUCKETS=16 FS_PARITY=1 STG_CODEC_LIB=$R/stellatrain_amd/libstg_codec_stamps.so \
+        prof_lfin_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_stamps.so step prof_lfin_stamps 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lfin_stamps" -o run -- python3 tools/lfin_probe.py ;;
+        lfin_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_stamps.so step lfin_stamps 200 python tools/lfin_probe.py ;;
+        fill_stamps) FS_BUCKETS=16 FS_PARITY=1 STG_CODEC_LIB=$R/tools/variants/libstg_codec_stamps.so \
                 step fill_stamps 200 python tools/fill_stamps.py ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
     esac

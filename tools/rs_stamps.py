@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase times of the radix select's first level (rs_hist<20,11>) inside a
 top-k call, from s_memrealtime stamps (100 MHz).  Needs the stamp build:
-make -C stellatrain_amd/csrc OUT=../libstg_codec_rsst.so BUILD=build_rsst EXTRA=-DSTG_RS_STAMPS=1,
+make -C stellatrain_amd/csrc OUT=../../tools/variants/libstg_codec_rsst.so BUILD=build_rsst EXTRA=-DSTG_RS_STAMPS=1,
 selected with STG_CODEC_LIB.  Prints, per call: the spread of workgroup starts,
 first start -> last streaming end, -> last flush, -> pick start, pick length."""
 import ctypes as C

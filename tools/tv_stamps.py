@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase times of one threshold-v launch (tv_pass) on C3 (256 MiB, k = 0.1 %),
 from s_memrealtime stamps (100 MHz).  Needs the stamp build:
-make -C stellatrain_amd/csrc OUT=../libstg_codec_tvst.so BUILD=build_tvst EXTRA=-DSTG_TV_STAMPS=1,
+make -C stellatrain_amd/csrc OUT=../../tools/variants/libstg_codec_tvst.so BUILD=build_tvst EXTRA=-DSTG_TV_STAMPS=1,
 selected with STG_CODEC_LIB.  Times are microseconds after the start of the
 workgroup that drew ticket 0: the last workgroup start, the last ticket in,
 range 0's streaming end, the last streaming end, the last look-back end, the

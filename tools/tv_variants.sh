@@ -8,6 +8,6 @@ make -s -j8
 while [ $# -ge 2 ]; do
     v=$1; f=$2; shift 2
     rm -rf build_$v && cp -a build build_$v && rm -f build_$v/${SRC:-tv.hip}.o
-    make -s -j8 BUILD=build_$v OUT=../libstg_codec_$v.so EXTRA="$f"
+    make -s -j8 BUILD=build_$v OUT=../../tools/variants/libstg_codec_$v.so EXTRA="$f"
     echo "built libstg_codec_$v.so ($f)"
 done
