@@ -9,10 +9,13 @@ tasks from several pool workers at once (engine/modules/compress.cpp:141,
 config.h:7); here the step is four batched C-ABI calls
 (stg_codec_compress_batch_device) of 4 buckets each on four streams = four
 concurrent persistent launches, so one launch's tail and regime-B heap fill
-overlap the others' streaming.  Each rank holds 2 buffer sets (the engine's iter%2 shm
-buffers, core.cpp:967) = 32 distinct buckets (2 GiB >> the 256 MB Infinity
-Cache); step s compresses set s%2, so every key sees fresh data each visit and
-its AIMD threshold runs its real regime A/B sequence.  Keys are initialised
+overlap the others' streaming.  Each rank holds 8 buffer sets of its 16
+buckets (8 GiB, >> the 256 MB Infinity Cache; --sets): step s compresses set
+s % 8, so every key sees a fresh bucket on every step (the engine
+alternates two shm buffers per layer, core.cpp:967, whose contents are fresh
+each iteration) and its AIMD threshold runs its real regime A/B sequence.
+``--jitter J`` scales each bucket by a seeded factor in [1 - J, 1 + J], so
+that AIMD window misses happen at a gradient-noise rate.  Keys are initialised
 (first-threshold call) before the warmup.  value = 16 x 64 MiB x steps / time.
 
 N > 1: the same step on every rank (each its own 16 keys and buckets, seeded
@@ -86,6 +89,12 @@ def parse():
     p.add_argument("--streams", type=int, default=4,
                    help="issue batch j on stream j %% S, like the engine's worker pool; S persistent launches "
                         "share the chip")
+    p.add_argument("--sets", type=int, default=8,
+                   help="buffer sets rotated over the steps: each key sees a fresh bucket on every step for "
+                        "SETS steps running (SURVEY 8(d)); 8 x 16 x 64 MiB = 8 GiB per GPU")
+    p.add_argument("--jitter", type=float, default=0.0,
+                   help="scale each (key, set) bucket by a seeded factor in [1 - J, 1 + J] (gradient-scale "
+                        "noise: AIMD window misses at a realistic rate)")
     p.add_argument("--master-port", type=int, default=29517)
     return p.parse_args()
 
@@ -165,6 +174,25 @@ def cpu_baseline(n: int, k: int, seconds: float):
             "sample": f"thresholdv16 {4 * n >> 20} MiB k={k}: {T} threads x distinct keys, {cT} steady-state calls "
                       f"in {dT:.1f} s ({c1} calls in {d1:.1f} s on 1 thread); 2 alternating synthetic buckets per "
                       f"key, first call excluded; {src}"}
+
+
+def jitter_factor(bucket: int, par: int, jitter: float) -> float:
+    """A seeded factor in [1 - jitter, 1 + jitter] for (bucket, set): the
+    splitmix64 of synth.py, so every run and world size sees the same inputs."""
+    from stellatrain_amd.synth import _splitmix64, seed_for
+    r = int(_splitmix64(np.array([seed_for(bucket, par) ^ 0x7A11], np.uint64))[0]) >> 11
+    return float(1.0 + jitter * (2.0 * r / float(1 << 53) - 1.0))
+
+
+def fill_profile():
+    """tv16_fill per-launch durations (p50 / p99 / max) from the committed
+    rocprofv3 kernel trace summary of the headline (profiles/fill_profile.json,
+    written by tools/fill_profile.py)."""
+    path = os.path.join(ROOT, "profiles", "fill_profile.json")
+    try:
+        return json.load(open(path))
+    except Exception:
+        return None
 
 
 def load_traffic(buckets_per_launch: int):
@@ -331,14 +359,19 @@ def main():
     stream = torch.cuda.current_stream(dev)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
 
-    # 2 buffer sets (iter % 2), data seeded by bucket id: identical for any world size
+    # args.sets buffer sets rotated over the steps (each key sees a fresh bucket
+    # on every step), data seeded by bucket id and set: identical for any world
+    # size; --jitter scales each (bucket, set) by a seeded factor
     tot = sum(n for _, n, _, _ in items)
     offs = np.concatenate([[0], np.cumsum([n for _, n, _, _ in items])]).astype(np.int64)
-    sets = [torch.empty(max(tot, 1), dtype=torch.float32, device=dev) for _ in range(2)]
-    for par in range(2):
+    nsets = max(1, args.sets)
+    sets = [torch.empty(max(tot, 1), dtype=torch.float32, device=dev) for _ in range(nsets)]
+    for par in range(nsets):
         for j, (_, n, _, b) in enumerate(items):
             check(lib().stg_synth_fill_device(C.c_void_p(sets[par][offs[j]:].data_ptr()), n, seed_for(b, par), 0, 0,
                                               C.c_void_p(stream.cuda_stream)))
+            if args.jitter > 0:
+                sets[par][offs[j]:offs[j] + n].mul_(jitter_factor(b, par, args.jitter))
     ks = [k for _, _, k, _ in items]
     koffs = np.concatenate([[0], np.cumsum(ks)]).astype(np.int64)
     oidx = torch.zeros(max(sum(ks), 1), dtype=torch.int32, device=dev)
@@ -352,7 +385,7 @@ def main():
     else:
         groups = [list(range(j, min(j + 16, nb))) for j in range(0, nb, 16)]
     plans = []
-    for par in range(2):
+    for par in range(nsets):
         calls = []
         for j, g in enumerate(groups):
             rows = [(items[i][0].encode(), sets[par][offs[i]:].data_ptr(), items[i][1], ks[i],
@@ -362,7 +395,7 @@ def main():
         plans.append(calls)
 
     def step(s):
-        for arr, n_, sp in plans[s % 2]:
+        for arr, n_, sp in plans[s % nsets]:
             comp.compress_batch_raw(arr, n_, sp)
 
     def sync_streams():
@@ -467,8 +500,10 @@ def main():
             "scaling": "weak" if wl == "headline" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic (splitmix64 Irwin-Hall D1, 2 buffer sets of {nb} distinct buckets per GPU, device "
-                    "resident)",
+            "data": f"synthetic (splitmix64 Irwin-Hall D1, {nsets} buffer sets of {nb} distinct buckets per GPU "
+                    f"rotated over the steps: a fresh bucket per key every step"
+                    + (f", each scaled by a seeded factor in [{1 - args.jitter:g}, {1 + args.jitter:g}]"
+                       if args.jitter > 0 else "") + ", device resident)",
             "config": dict(desc, streams=ns, buckets_per_launch=round(per_launch, 2),
                            parallelism=f"bucket-sharded x{world}, no collective"),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -476,7 +511,11 @@ def main():
                          "traffic": load_traffic(per_launch) if wl == "headline" else None,
                          "kernel": "tv16_batch", "alg_bytes_per_launch": int(alg_step / max(len(groups), 1)),
                          "pitch_us": round(pitch_us, 2), "concurrent_launches": conc, "launches_timed": int(launches),
-                         "interval_us": round(chip_ms * 1e3, 1), "rank": 0},
+                         "interval_us": round(chip_ms * 1e3, 1), "rank": 0,
+                         "basis": "step-level: algorithmic bytes of the profiled steps over their chip interval "
+                                  "(HIP events on stream 0, the other streams joined); the per-launch kernel "
+                                  "durations overlap (concurrent_launches in flight), so a per-kernel figure "
+                                  "cannot reproduce this frac"},
             "per_gpu_GBps": round(value / world, 2),
             "per_rank_GBps": per_rank_gbps,
             "rccl_world_size": dist.get_world_size() if world > 1 else 1,
@@ -489,6 +528,9 @@ def main():
                              for g in shard_meta]
             if args.dump_shards:
                 json.dump(shard_meta, open(args.dump_shards, "w"))
+        fp = fill_profile() if wl == "headline" else None
+        if fp:
+            out["fill_profile"] = fp
         if c4 is not None:
             out["c4"] = c4
         if world == 1 and not args.no_cpu_baseline and wl == "headline":
@@ -516,10 +558,12 @@ def main_oracle(args, world, rank):
     h = o.tv16_new()
 
     def timed(items_, steps):
-        data = [[o.synth(n, seed_for(b, par)) for (_, n, _, b) in items_] for par in range(2)]
+        nsets = max(1, args.sets)
+        data = [[o.synth(n, seed_for(b, par)) * np.float32(jitter_factor(b, par, args.jitter) if args.jitter > 0 else 1)
+                 for (_, n, _, b) in items_] for par in range(nsets)]
 
         def step(s):
-            return [o.tv16_compress(h, key, data[s % 2][j], k)[0] for j, (key, _, k, _) in enumerate(items_)]
+            return [o.tv16_compress(h, key, data[s % nsets][j], k)[0] for j, (key, _, k, _) in enumerate(items_)]
         step(0)
         for s in range(args.warmup):
             step(s + 1)

@@ -29,6 +29,11 @@ for s in "$@"; do
         tests_tv16) step tests_tv16 600 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_coresidency.py tests/test_gpu_fill_modes.py -v -m gpu --timeout 120 --timeout-method thread ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
         bench) step bench 400 python bench.py ;;
+        bench_jitter) step bench_jitter 400 python bench.py --jitter 0.05 --no-cpu-baseline ;;
+        prof_jitter) step prof_jitter 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_jitter" -o run \
+                -- python3 bench.py --steps 100 --warmup 8 --no-cpu-baseline --c4-sweeps 0 --jitter 0.05 ;;
+        prof_fresh) step prof_fresh 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_fresh" -o run \
+                -- python3 bench.py --steps 100 --warmup 8 --no-cpu-baseline --c4-sweeps 0 ;;
         bench_short) step bench_short 300 python bench.py --steps 40 --warmup 8 --cpu-seconds 5 ;;
         breakdown) step breakdown 300 python tools/breakdown.py ;;
         breakdown_d3) step breakdown_d3 300 python tools/breakdown.py --dist 2 --param 9000 ;;
