@@ -57,6 +57,7 @@ struct Workspace {
     size_t cap_sums = 0, cap_tiles = 0, cap_stage = 0, cap_desc = 0, cap_lone = 0;
     uint32_t epoch = 0;  // thresholdv16 call counter (hand-off tags)
     uint32_t tk_tag = 0; // one-launch top-k call counter (topk1.hip)
+    uint32_t lone_calls = 0;  // thresholdv16 one-bucket path calls (tv16.hip: parity of its per-call blocks)
     // threshold-v: the ticket's value at the next call, the last call's
     // range-descriptor tag and the descriptor block last zeroed (tile_cnt, its size)
     uint64_t tv_base = 0;
@@ -107,7 +108,8 @@ struct Workspace {
         const size_t o_cand = carve(sizeof(uint32_t) * stg::CAND_WORDS * stg::MAX_BATCH);
         const size_t o_misc = carve(sizeof(uint32_t) * 64);
         const size_t o_tvt = carve(sizeof(uint64_t));
-        const size_t o_wh = carve(sizeof(uint32_t) * stg::LNBIN);
+        const size_t o_wh = carve(sizeof(uint32_t) * 2 * stg::LNBIN);
+        const size_t o_larr = carve(sizeof(uint32_t) * stg::LARR_WORDS);
         const size_t o_we = carve(sizeof(uint2) * stg::LNBIN * stg::LBCAP);
         const size_t o_crew = carve(sizeof(stg::CrewCtl) * stg::MAX_BATCH);
         const size_t o_tkc = carve(sizeof(stg::TopkCtl) * 2);
@@ -126,6 +128,7 @@ struct Workspace {
         d.misc = reinterpret_cast<uint32_t *>(b + o_misc);
         d.tv_ticket = reinterpret_cast<uint64_t *>(b + o_tvt);
         d.whist = reinterpret_cast<uint32_t *>(b + o_wh);
+        d.larr = reinterpret_cast<uint32_t *>(b + o_larr);
         d.went = reinterpret_cast<uint2 *>(b + o_we);
         d.crew = reinterpret_cast<stg::CrewCtl *>(b + o_crew);
         d.tkctl = reinterpret_cast<stg::TopkCtl *>(b + o_tkc);
@@ -430,6 +433,7 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
                      : (uint32_t)(2 * h->num_cu);
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     a.lone_cap = (uint32_t)ws->cap_lone;
+    a.lone_calls = &ws->lone_calls;
     if (!inflight && !tv16_serial()) {  // no admission: nothing to track
         HIP_TRY(stg::launch_tv16(a, ws->d, s));
         grp.clear();

@@ -846,6 +846,43 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         L.whist = ws.whist;
         L.went = ws.went;
         L.zero_next = reinterpret_cast<uint32_t *>(&ws.ctl->cc[(a.epoch + 1) & 1u]);
+        // the window histogram and the finish's arrival block by call parity:
+        // this call's copies were zeroed by the previous call's scan
+        uint32_t tag = a.epoch;
+        if (a.lone_calls) {
+            if (++*a.lone_calls == 0) *a.lone_calls = 2;  // (0 is never a tag; the parity keeps alternating)
+            tag = *a.lone_calls;
+        }
+        const uint32_t par = tag & 1u;
+        L.whist = ws.whist + (size_t)par * LNBIN;
+        L.whist_next = ws.whist + (size_t)(par ^ 1u) * LNBIN;
+        L.tag = tag;
+        L.done = ws.larr;
+        L.tl = (uint32_t)(a.b[0].n % 16);
+        // the finish inside the scan launch (tv16lf2.h): not under the fused
+        // gather (the scan rewrites the bucket) or the wire form
+        static const int lf2_env = getenv("STG_TV16_LF2") ? atoi(getenv("STG_TV16_LF2")) : 1;
+        static const uint32_t lf2_fin = (uint32_t)std::max(0, std::min(
+            getenv("STG_TV16_LF2_FIN") ? atoi(getenv("STG_TV16_LF2_FIN")) : 64, (int)LF2_MAXF));
+        static const uint32_t lf2_wk = (uint32_t)std::max(8, std::min(
+            getenv("STG_TV16_LF2_WORKERS") ? atoi(getenv("STG_TV16_LF2_WORKERS")) : 48, (int)LF2_MAXF));
+        {
+            static const uint32_t fill_mode0 =
+                getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
+            const bool lf2 = lf2_env != 0 && !fused_gather && !a.b[0].wflag && lf2_fin > lf2_wk;
+            L.fin = lf2 ? lf2_fin : 0u;
+            L.nwk = lf2_wk;
+            L.mode = fill_mode0;
+            L.out_idx = a.b[0].idx;
+            L.out_val = a.b[0].val;
+            L.count_out = a.b[0].count_out;
+            L.dst_len = a.b[0].dst_len;
+            L.idx_offset = a.b[0].idx_offset;
+            L.fail = ws.fail;
+            L.dbg = ws.misc;
+            static const uint32_t skip = getenv("STG_LF2_SKIP") ? (uint32_t)atoi(getenv("STG_LF2_SKIP")) : 0u;
+            L.skip = skip;
+        }
         if (fused_gather) {  // (fused_gather: bucket 0's gather has a term to add)
             const GatherArgs &g = *a.b[0].gather;
             L.gres = g.resid;
@@ -853,7 +890,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             L.gn = std::max<uint32_t>(1, g.nsrc);
             L.tl = (uint32_t)(a.b[0].n % 16);
         }
-        hipError_t e = launch_tv16_lscan(L, a.num_cu, s);
+        hipError_t e = launch_tv16_lscan(L, a.num_cu, s);  // (clamps L.fin to what the grid allows)
         if (e != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[1], s);
         if (a.scan_done && (e = hipEventRecord(a.scan_done, s)) != hipSuccess) return e;
@@ -883,14 +920,20 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.lq = ws.lq;
         F.lw = ws.lw;
         F.lv = ws.lv;
-        F.whist = ws.whist;
+        F.whist = L.whist;
         F.went = ws.went;
         F.state = a.b[0].state;
         F.cp = ws.cp;
         F.resid = a.b[0].resid;
+        F.fin = L.fin;
+        F.fin_tag = L.tag;
+        F.fin_done = L.done;
         F.crew = crew_lone(a.num_cu, workers + rankers);
         F.crew_ctl = ws.crew;
         if ((e = launch_tv16_fill_any(F, s)) != hipSuccess) return e;
+        static const uint32_t noop_g = getenv("STG_DEBUG_NOOP") ? (uint32_t)atoi(getenv("STG_DEBUG_NOOP")) : 0u;
+        static const uint32_t noop_lds = getenv("STG_DEBUG_NOOP_LDS") ? (uint32_t)atoi(getenv("STG_DEBUG_NOOP_LDS")) : 0u;
+        if (noop_g && (e = launch_lone_noop(noop_g, noop_lds, ws.fail, ws.misc + 63, s)) != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[2], s);
         return hipGetLastError();
     }

@@ -100,5 +100,20 @@ __device__ __forceinline__ void gather16(const void *src, uint32_t n16, void *ds
     vm_drain();
 }
 
+// Heap positions of libstdc++'s make_heap (node q = pos + 1 >= 1).
+__device__ __forceinline__ uint32_t depth_of(uint32_t q) { return 31u - __clz(q); }
+// right-first pre-order key of heap position pos (< 2^20 - 1): ancestors
+// first, then the right subtree before the left one
+__device__ __forceinline__ uint32_t rf_key(uint32_t pos) {
+    const uint32_t q = pos + 1, d = depth_of(q);
+    const uint32_t path = q - (1u << d);
+    const uint32_t inv = ~path & ((1u << d) - 1u);
+    return ((inv << (19u - d)) << 5) | d;
+}
+__device__ __forceinline__ bool is_desc(uint32_t q, uint32_t qt) {  // heap node q (pos + 1) below node qt
+    const uint32_t dp = depth_of(q), dt = depth_of(qt);
+    return dp > dt && (q >> (dp - dt)) == qt;
+}
+
 }  // namespace tv16
 }  // namespace stg

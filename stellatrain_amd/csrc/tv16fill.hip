@@ -85,7 +85,6 @@ static_assert(NBIN << 8 == TV16_WIN, "output-sort bins of 256 ulps cover the win
 // A heap node as a DFS key: its path from the root left-aligned to depth 19
 // (20 bits) << 5 | its depth.  Ascending keys = pre-order, left subtree first;
 // ancestors come before their descendants.
-__device__ __forceinline__ uint32_t depth_of(uint32_t q) { return 31u - __clz(q); }  // q = pos + 1 >= 1
 __device__ __forceinline__ uint32_t dkey_of_pos(uint32_t pos) {
     const uint32_t q = pos + 1, d = depth_of(q);
     return ((q << (19u - d)) << 5) | d;
@@ -204,14 +203,6 @@ __device__ void counting_sort(SortScratch &X, uint16_t *out, uint32_t *sh, uint3
     __syncthreads();
 }
 
-// right-first pre-order key of heap position pos (< 2^20 - 1): ancestors
-// first, then the right subtree before the left one
-__device__ __forceinline__ uint32_t rf_key(uint32_t pos) {
-    const uint32_t q = pos + 1, d = depth_of(q);
-    const uint32_t path = q - (1u << d);
-    const uint32_t inv = ~path & ((1u << d) - 1u);
-    return ((inv << (19u - d)) << 5) | d;
-}
 
 // Emit the lines / tail of the output order: entry i of the order goes to
 // offset cnt + 16 i (less 16 - tl after the tail), at most rem elements.  Four
@@ -556,6 +547,8 @@ tv16_fill(Tv16FillArgs A) {
     // emit a share of it (each waits only on a workgroup already running)
     __shared__ uint32_t s_role, s_last;
     const uint32_t tid = threadIdx.x;
+    // a one-bucket call its scan launch finished (tv16lf2.h): nothing to do
+    if (LONE && A.fin && !__syncthreads_or(tid < A.fin && A.fin_done[tid] != A.fin_tag)) return;
     if (!LONE && blockIdx.x >= A.nbk) {  // the crew (tv16wide.h)
         crew_from_decisions<LONE>(*reinterpret_cast<WideLds *>(fill_lds), S, A);
         return;

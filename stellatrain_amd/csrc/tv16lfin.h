@@ -129,9 +129,9 @@ __device__ __forceinline__ void lfin_prefix(LfinLds &L, const LfinArgs &A, LfinD
 #pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
         const uint32_t c = tid * PER + u;
-        const uint2 x = c < nc ? A.ldesc[c] : make_uint2(0u, 0u);
-        qv[u] = x.x;
-        wv[u] = x.y;
+        const uint2 x = c < nc ? A.ldesc[c] : make_uint2(0u, 0u);  // {qualifying:16 | window:16, call tag}
+        qv[u] = x.x & 0xffffu;
+        wv[u] = x.x >> 16;
     }
 #pragma unroll
     for (uint32_t u = 0; u < PER; ++u) {
@@ -349,10 +349,6 @@ __device__ __noinline__ void lfin_list(LfinLds &L) {
 // ---------------------------------------------------------------------------
 // ranker `rk`: the regime-B fill's order for a share of the kept lines
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool is_desc(uint32_t q, uint32_t qt) {  // heap node q (pos + 1) below node qt
-    const uint32_t dp = depth_of(q), dt = depth_of(qt);
-    return dp > dt && (q >> (dp - dt)) == qt;
-}
 
 __device__ __noinline__ void lfin_ranker(LfinLds &L, uint32_t rk) {
     const LfinArgs &A = L.args;

@@ -53,7 +53,13 @@ using namespace tv16;
 static_assert(LCHUNK <= 512 && LMAXC <= 4096 && LQCAP < 1024, "binned entry packing: chunk:12 | line:9 | qb:10");
 static_assert(LNBIN << 8 == TV16_WIN, "bins of 256 ulps cover the window");
 
+#ifndef STG_LSCAN_PAD
+#define STG_LSCAN_PAD 0  // diagnostics: extra LDS bytes per workgroup (occupancy A/B)
+#endif
 struct LLds {
+#if STG_LSCAN_PAD
+    uint32_t pad_[STG_LSCAN_PAD / 4];
+#endif
     float4 qv[2][LQCAP][4];  // their data (a float4 per lane of the line's quad)
     uint32_t ql[2][LQCAP];  // qualifying lines of the chunk in the slot (unordered)
     uint64_t wl[2][LWCAP];  // window lines: sum bits << 32 | line
@@ -79,6 +85,11 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
     uint32_t *lq = A.lq + (size_t)c * LQCAP;
     uint2 *lw = A.lw + (size_t)c * LWCAP;
     float4 *lv = A.lv + (size_t)c * LQCAP * 4;
+    // lq, lv, went and the counts are read inside this launch by the finish
+    // (tv16lf2.h): written through (sc1), as the hand-off requires
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(lq, 0, LQCAP * 4u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(lv, 0, LQCAP * 64u, 0x00020000);
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(A.went, 0, LNBIN * LBCAP * 8u, 0x00020000);
     // entry e of the list has rank r_e; its line data (four float4) goes to
     // lv[r_e]: lane = 16 entries x 4 quarters per round
     for (uint32_t e0 = 0; e0 < ql; e0 += 16) {
@@ -87,8 +98,11 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
             const uint32_t li = L.ql[sl][e];
             uint32_t r = 0;
             for (uint32_t x = 0; x < ql; ++x) r += L.ql[sl][x] < li;
-            if (qq == 0) lq[r] = li;
-            lv[r * 4 + qq] = L.qv[sl][e][qq];
+            if (qq == 0) __builtin_amdgcn_raw_buffer_store_b32(li, rq, r * 4u, 0, 16 /* sc1 */);
+            const float4 x = L.qv[sl][e][qq];
+            u4v t4;
+            t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
+            __builtin_amdgcn_raw_buffer_store_b128(t4, rv, (r * 4u + qq) * 16u, 0, 16 /* sc1 */);
         }
     }
     if (wlc) {  // at most one entry per lane
@@ -97,11 +111,20 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
         for (uint32_t x = 0; x < wlc; ++x) r += (uint32_t)L.wl[sl][x] < li;
         for (uint32_t x = 0; x < ql; ++x) qb += L.ql[sl][x] < li;
         if (lane < wlc) {
-            lw[r] = make_uint2((uint32_t)(we >> 32), li | qb << 16);
-            if (wslot < LBCAP) A.went[wbin * LBCAP + wslot] = make_uint2((uint32_t)(we >> 32), c << 19 | li << 10 | qb);
+            st_sc1(reinterpret_cast<uint64_t *>(lw + r), (uint64_t)(li | qb << 16) << 32 | (uint32_t)(we >> 32));
+            if (wslot < LBCAP) {
+                typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+                u2v t2;
+                t2.x = (uint32_t)(we >> 32);
+                t2.y = c << 19 | li << 10 | qb;
+                __builtin_amdgcn_raw_buffer_store_b64(t2, re, (wbin * LBCAP + wslot) * 8u, 0, 16 /* sc1 */);
+            }
         }
     }
-    if (lane == 0) A.ldesc[c] = make_uint2(qn, wn);
+    // the chunk's counts, tagged with the call: the finish (tv16lf2.h) waits
+    // for every chunk's tag; the lists above are drained first
+    vm_drain();
+    if (lane == 0) st_sc1(reinterpret_cast<uint64_t *>(A.ldesc) + c, (uint64_t)A.tag << 32 | wn << 16 | qn);
     lds_drain();
     if (lane == 0) {
         L.qn[sl] = 0;
@@ -117,9 +140,18 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
 // residual, then grad[1] .. grad[N-1]) are read beside the bucket, summed into
 // it in gather.hip's order, and the sum is stored back once (grad[0] ends as
 // the gather-add leaves it) and is what the line sums see.
+#include "tv16lf2.h"
+
+union LScanLds {
+    LLds s;
+    Lf2Lds f;
+};
+static_assert(sizeof(LScanLds) <= 160 * 1024 / 8, "eight scan workgroups per CU");
+
 template <bool EF, uint32_t NW, uint32_t D, uint32_t GS>
-__global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
-    __shared__ LLds L;
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8, 8))) tv16_lscan(LScanArgs A) {
+    __shared__ LScanLds U;
+    LLds &L = U.s;
     const uint32_t tid = threadIdx.x;
     if (tid < 2) { L.qn[tid] = 0; L.wn[tid] = 0; L.done[tid] = 0; L.fin[tid] = 0; }
     // the extra streams in summation order: the residual, then grad[1] ..
@@ -136,6 +168,8 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
     }
     // the next call's counters (the finish of this call uses the other copy)
     if (blockIdx.x == 0 && tid < sizeof(CallCtl) / 4) st_sc1(A.zero_next + tid, 0u);
+    if (blockIdx.x == 0 && A.whist_next)  // the next call's window histogram
+        for (uint32_t i = tid; i < LNBIN; i += NW * 64) st_sc1(A.whist_next + i, 0u);
     const uint32_t s = uni(tid >> 6), lane = flane(), q = lane & 3u;
     const uint32_t lane_line = s * 16 + (lane >> 2);
     float t = 0.f;
@@ -199,11 +233,12 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
 #pragma unroll
             for (uint32_t e = 0; e < GS; ++e) w[e][u] = load_x(e, u);
         }
+        if (STG_LF2_STAMPS && j == 0 && blockIdx.x == 0 && tid == 0) A.dbg[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         if (j == 0) {  // the threshold, read while the chunk's first loads are in flight
             t = uni(A.state->t);
             if (blockIdx.x == 0 && tid == 0) {  // the finish decides with the threshold the scan used
-                A.cp->t = t;
-                A.cp->inc = A.state->inc;
+                st_sc1(reinterpret_cast<uint32_t *>(&A.cp->t), f2u(t));
+                st_sc1(reinterpret_cast<uint32_t *>(&A.cp->inc), f2u(A.state->inc));
             }
             tb = f2u(t);
             wlo = tb > TV16_WIN ? tb - TV16_WIN : 0u;  // window [wlo, tb) just below t
@@ -287,12 +322,28 @@ __global__ void __launch_bounds__(NW * 64) tv16_lscan(LScanArgs A) {
             }
         }
     }
+    if (!STG_LSCAN_DIAG && A.fin && blockIdx.x + A.fin >= gridDim.x) lf2_finish(U.f, A, blockIdx.x + A.fin - gridDim.x);
+}
+
+// diagnostics (STG_DEBUG_NOOP): a launch whose workgroups read one word and
+// exit, to price a follow-on launch that has nothing to do
+__global__ void lone_noop(const uint32_t *w, uint32_t *out) {
+    extern __shared__ uint32_t noop_lds[];
+    if (threadIdx.x == 0 && ld_sc1(w) == 0x12345678u) { noop_lds[0] = 1; out[0] = noop_lds[0]; }
 }
 
 }  // namespace
 
-hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s) {
-    if (!a.nc) return hipSuccess;
+hipError_t launch_lone_noop(uint32_t grid, uint32_t lds, const uint32_t *w, uint32_t *out, hipStream_t s) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&lone_noop),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    lone_noop<<<grid, 512, lds, s>>>(w, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tv16_lscan(LScanArgs &a, int num_cu, hipStream_t s) {
+    if (!a.nc) { a.fin = 0; return hipSuccess; }
     // shape (diagnostics: STG_TV16_LSHAPE): 0 = 4 waves, 8 float4 loads in
     // flight per lane (the whole 32 KiB chunk), eight workgroups per CU (the
     // fastest single-launch 64 MiB read measured, tools/ubench_stream.hip);
@@ -301,6 +352,9 @@ hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s) {
     const bool ef = a.resid != nullptr;
     const uint32_t per_cu = shape == 1 ? 4u : 8u;
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(a.nc, per_cu * (uint32_t)num_cu));
+    // the finish's roles: the last `fin` workgroups of the grid, at least
+    // nwk + 1 of them (a ranker); else the fill launch finishes the call
+    if (a.fin && (G < 2 * a.fin || a.fin <= a.nwk || a.nwk < 8 || a.nc > LMAXC || a.gn || !a.tag)) a.fin = 0;
     if (a.gn) {  // the gather fused: fewer loads in flight per stream, more streams
         const uint32_t ns = (a.gres ? 1u : 0u) + a.gn - 1u;
         if (a.gn > GATHER_MAX) return hipErrorInvalidValue;

@@ -159,7 +159,8 @@ struct DevWS {
     uint32_t *lq;        // ... the chunk's qualifying lines in order (LQCAP per chunk, line within the chunk)
     uint2 *lw;           // ... its window lines in order: {sum bits, line within the chunk | qualifying before << 16}
     float4 *lv;          // ... the qualifying lines' data (LQCAP x 4 float4 per chunk)
-    uint32_t *whist;     // ... window entries per bin (LNBIN, zero between calls)
+    uint32_t *whist;     // ... window entries per bin (2 x LNBIN by call parity, zero between calls)
+    uint32_t *larr;      // ... the scan's finish: per role the tag of the last call it finished
     uint2 *went;         // ... the entries by bin (LNBIN x LBCAP)
 };
 
@@ -198,6 +199,8 @@ struct Tv16Launch {
     uint32_t desc_cap;   // ChunkDesc entries at ws.desc
     hipEvent_t scan_done;  // optional: recorded between the scan and the fill launch
     uint32_t lone_cap;   // chunks the one-bucket lists (ws.ldesc / lq / lw) hold (0: none)
+    uint32_t *lone_calls;  // the workspace's one-bucket path calls (host; its parity picks the
+                           // window histogram and arrival block, each call zeroing the other copy)
 };
 hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s);
 // thresholdv16 regime-B heap fill (tv16fill.hip): one workgroup per bucket
@@ -237,12 +240,16 @@ struct Tv16FillArgs {
     const uint32_t *lq;
     const uint2 *lw;
     const float4 *lv;
-    uint32_t *whist;       // the scan's binned window (counts zeroed by the last workgroup)
+    uint32_t *whist;       // the scan's binned window (this call's copy; the scan zeroes the next call's)
     const uint2 *went;
     uint32_t rankers;      // workgroups that order the regime-B fill in parallel (0: the orderer alone)
     KeyState *state;
     const CallParams *cp;  // {t, inc} as the scan read them
     float *resid;          // fused error feedback: the ragged tail is copied by the finish
+    // the scan launch finished the call (tv16lf2.h): every role of this launch
+    // leaves when fin_done[0 .. fin) all hold fin_tag (fin == 0: never)
+    const uint32_t *fin_done;
+    uint32_t fin, fin_tag;
 };
 hipError_t launch_tv16_fill(const Tv16FillArgs &a, hipStream_t s);
 // the same fill built to write the wire form of buckets with wflag set (tv16fill.hip)
@@ -254,11 +261,13 @@ inline hipError_t launch_tv16_fill_any(const Tv16FillArgs &a, hipStream_t s) {
 }
 // one-bucket scan (tv16lone.hip): every workgroup streams its chunks and lists
 // them; nothing waits on another workgroup
+constexpr uint32_t LF2_MAXF = 64;                     // finish roles of a one-bucket scan at most (tv16lf2.h)
+constexpr uint32_t LARR_WORDS = LF2_MAXF;             // per role: the call tag once its part is written
 struct LScanArgs {
     const float *src;
     uint32_t nb;           // full lines
     uint32_t nc;           // chunks
-    const KeyState *state;
+    KeyState *state;
     CallParams *cp;        // receives {t, inc} as read
     float *resid;          // fused error feedback (or null)
     uint2 *ldesc;
@@ -273,9 +282,24 @@ struct LScanArgs {
     const float *gres;     // residual term (null: none)
     const float *gsrc[GATHER_MAX];
     uint32_t gn;           // 0: no gather; else N (gsrc[0] unused)
-    uint32_t tl;           // the ragged tail's floats (summed by workgroup 0)
+    uint32_t tl;           // the ragged tail's floats (summed by workgroup 0 under the gather)
+    // the finish inside the scan launch (tv16lf2.h): `fin` roles (0: none, the
+    // fill launch finishes), `nwk` of them workers; arrival block of this call
+    // and of the next (zeroed here), and the next call's window histogram
+    uint32_t fin, nwk, mode;
+    uint32_t tag;          // the call's tag (>= 1) on every chunk's counts
+    uint32_t skip;         // diagnostics (STG_LF2_SKIP): a role stops at that point
+    uint32_t *done;        // per role: the tag once its part is written (LARR_WORDS)
+    uint32_t *whist_next;
+    uint32_t *out_idx;
+    float *out_val;
+    uint32_t *count_out;
+    uint32_t dst_len;
+    int32_t idx_offset;
+    uint32_t *fail, *dbg;
 };
-hipError_t launch_tv16_lscan(const LScanArgs &a, int num_cu, hipStream_t s);
+hipError_t launch_tv16_lscan(LScanArgs &a, int num_cu, hipStream_t s);
+hipError_t launch_lone_noop(uint32_t grid, uint32_t lds, const uint32_t *w, uint32_t *out, hipStream_t s);
 
 struct TvLaunch {
     const float *src;

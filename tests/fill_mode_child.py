@@ -84,6 +84,7 @@ def main():
     w = (C.c_uint32 * 64)()
     check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
     print(json.dumps({"ok": True, "calls": calls, "paths": list(w)[56:60], "lfin": list(w)[48:52],
+                      "scan_ranked": list(w)[44:46],
                       "wide": list(w)[52:56], "mode": os.environ.get("STG_DEBUG_TV16_FILL")}), flush=True)
 
 

@@ -37,10 +37,25 @@ def _child(mode: int, **extra):
 
 
 def test_production_order(gpu):
-    """One-bucket calls: the one-bucket finish's rankers order the regime-B
-    fills (tv16lfin.h); D1's regime-B calls tie among the pops.  The scale
-    drops are window misses: the crew orders them, never the literal heap."""
+    """One-bucket calls: the scan launch's finish (tv16lf2.h) ranks the
+    regime-B fills; D1's regime-B calls tie among the pops.  The scale drops
+    are window misses: the fill launch's crew orders them, never the literal
+    heap."""
     out = _child(0)
+    plain, tied, viol, notake = out["lfin"]
+    assert out["scan_ranked"][1] > 0, out  # ranked with ties in the scan launch
+    assert out["paths"][3] == 0, out  # never the literal heap
+    leader, crew, leader_lit, crew_lit = out["wide"]
+    assert crew > 0 and leader_lit == 0 and crew_lit == 0, out
+
+
+@pytest.mark.parametrize("env", [{"STG_TV16_LF2": "0"}, {"STG_LF2_SKIP": "1"}, {"STG_LF2_SKIP": "4"}],
+                         ids=["lfin_only", "scan_rankers_give_up", "scan_workers_give_up"])
+def test_production_order_fill_finish(gpu, env):
+    """The fill launch's finish (tv16lfin.h): with the scan's finish off, or
+    with its rankers / workers giving up (STG_LF2_SKIP), the fill launch's
+    rankers order the regime-B fills (with ties), bit-exact as before."""
+    out = _child(0, **env)
     plain, tied, viol, notake = out["lfin"]
     assert tied > 0, out
     assert out["paths"][3] == 0, out  # never the literal heap
@@ -51,7 +66,7 @@ def test_production_order(gpu):
 def test_production_order_orderer_alone(gpu):
     """The one-bucket finish without rankers: its last workgroup runs the
     orderer (tv16fill.hip) on every regime-B call."""
-    out = _child(0, STG_TV16_LFIN_RANKERS="0")
+    out = _child(0, STG_TV16_LFIN_RANKERS="0", STG_TV16_LF2="0")
     none, by_start, shadow, literal = out["paths"]
     assert by_start > 0 and literal == 0, out
     assert out["lfin"] == [0, 0, 0, 0], out
