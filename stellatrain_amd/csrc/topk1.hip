@@ -712,7 +712,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
                     L.v[9] = ld_sc1(&C->tk[p][s][0]) >= su ? su : g_add(&C->tk[p][s][0], 1u);
                 __syncthreads();
                 const uint32_t c = L.v[9];
-                if (c >= su) { __syncthreads(); break; }
+                if (c >= su) { __syncthreads(); break; }  // uniform: c is read from LDS after a barrier
                 const uint32_t tile = s + TK1_SH * c;
                 if (p == M_H1) unit_hist<VEC, 20, 11>(A, L, tile);
                 else if (p == M_H2) unit_hist<VEC, 9, 11>(A, L, tile);

@@ -151,13 +151,16 @@ __device__ __forceinline__ void lf2_decide(Lf2Lds &L, Lf2Dec &D, uint32_t (&h)[4
     const float i0 = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(&A.cp->inc)));
     for (uint32_t h0 = 0; h0 * RH * LF2_WG < nc; ++h0) {
         uint64_t x[RH];
+#pragma unroll
+        for (uint32_t u = 0; u < RH; ++u) x[u] = 0;
         uint64_t st = 0;
         for (uint32_t sp = 0;; ++sp) {  // until every chunk of the round carries this call's tag
-            uint32_t miss = 0;
+            uint32_t miss = 0;          // (a poll reloads only the chunks not yet seen listed)
 #pragma unroll
             for (uint32_t u = 0; u < RH; ++u) {
                 const uint32_t c = tid + (h0 * RH + u) * LF2_WG;
-                x[u] = c < nc ? ld_sc1(reinterpret_cast<const uint64_t *>(A.ldesc) + c) : (uint64_t)A.tag << 32;
+                if ((uint32_t)(x[u] >> 32) != A.tag)
+                    x[u] = c < nc ? ld_sc1(reinterpret_cast<const uint64_t *>(A.ldesc) + c) : (uint64_t)A.tag << 32;
                 miss |= (uint32_t)(x[u] >> 32) != A.tag ? 1u : 0u;
             }
             if (!__syncthreads_or((int)miss)) break;

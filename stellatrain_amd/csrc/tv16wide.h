@@ -978,7 +978,7 @@ __device__ __noinline__ void crew_loop(WL &W, FillLds &S, const CrewArgs A) {
             crew_a<LONE ? CW_DA_LONE : CW_DA>(W, B, ctl, rel);
         } else if (p == 2) {  // C
             if (!crew_c(W, B, ctl, rel, A.epoch)) { poison(); return; }
-        } else if (p == 3) {  // D: the leader, or the literal heap
+        } else if (p == 3) {  // D: the leader, or the literal heap (uniform: p from the ticket in LDS)
             const CrewMap cm = crew_map(B);
             const uint32_t nL = ld_sc1(&ctl->nL), ovf = ld_sc1(&ctl->status), beta = ld_sc1(&ctl->beta);
             LeadIn I;
@@ -1004,7 +1004,7 @@ __device__ __noinline__ void crew_loop(WL &W, FillLds &S, const CrewArgs A) {
             O.tail_rank = NONE;
             O.ordpos = cm.keys;
             O.order = cm.keys;
-            if (STG_CREW_STAMPS >= 2 && !ovf) {  // diagnostics: a first run warms the caches
+            if (STG_CREW_STAMPS >= 2 && !ovf) {  // diagnostics: a first run warms the caches (uniform: a final word)
                 (void)leader(W, I);
                 __syncthreads();
                 if (tid == 0) A.dbg[29] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -1018,7 +1018,7 @@ __device__ __noinline__ void crew_loop(WL &W, FillLds &S, const CrewArgs A) {
                 st_sc1(&ctl->tail_rank, O.tail_rank);
                 st_sc1(&ctl->op, ok ? (uint32_t)(O.order - cm.keys) : 0u);
             }
-            if (!ok) {  // exact, slow; its LDS view covers this workgroup's plan, so it takes no more units
+            if (!ok) {  // exact, slow; its LDS view covers this workgroup's plan, so it takes no more units (uniform: the leader's result)
                 const CrewBk Bl = B;
                 __syncthreads();
                 full_path(S, Bl.d, Bl.cnt, Bl.N, u2f(Bl.tbits), Bl.tail != 0, u2f(Bl.tail_bits), A.fail);

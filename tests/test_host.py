@@ -150,3 +150,50 @@ def test_new_entry_points_reject_bad_arguments_without_gpu():
         arr = (StgBucket * 1)()
         assert L.stg_merge_compress_batch_device(hc, arr, None, 1, None) == -1
         L.stg_codec_destroy(hc)
+
+
+def _barriers_under_branches_in_ticket_loops(src: str):
+    """(line, condition) of every `if` inside a `for (;;)` loop body whose
+    block holds a __syncthreads() (comments stripped first)."""
+    import re
+    nc = re.sub(r'//[^\n]*', lambda m: ' ' * len(m.group(0)), src)
+    nc = re.sub(r'/\*.*?\*/', lambda m: re.sub(r'[^\n]', ' ', m.group(0)), nc, flags=re.S)
+
+    def match(text, i, op, cl):  # index just past the bracket closing the one opened before i
+        d = 1
+        while d and i < len(text):
+            d += (text[i] == op) - (text[i] == cl)
+            i += 1
+        return i
+    out = []
+    for m in re.finditer(r'for\s*\(\s*;\s*;\s*\)\s*\{', nc):
+        start = m.end()
+        body = nc[start:match(nc, start, '{', '}')]
+        for im in re.finditer(r'\bif\s*\(', body):
+            j = match(body, im.end(), '(', ')')
+            k = j
+            while k < len(body) and body[k] in ' \t\n':
+                k += 1
+            blk = body[k:match(body, k + 1, '{', '}')] if k < len(body) and body[k] == '{' else body[k:body.find(';', k)]
+            if '__syncthreads' in blk:
+                out.append((nc[:start + im.start()].count('\n') + 1, body[im.start():j].strip()))
+    return out
+
+
+def test_no_unmarked_barrier_under_branch_in_ticket_loops():
+    """A __syncthreads() under a branch inside a `for (;;)` ticket loop hung
+    the first hinted Top-k call (Top-k).  Every such site must carry
+    a `uniform:` comment on its `if` line saying why the condition is the same
+    in every thread of the workgroup."""
+    import glob
+    csrc = os.path.join(ROOT, "stellatrain_amd", "csrc")
+    bad = []
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+        src = open(f).read()
+        lines = src.splitlines()
+        for ln, cond in _barriers_under_branches_in_ticket_loops(src):
+            if "uniform:" not in lines[ln - 1]:
+                bad.append(f"{os.path.basename(f)}:{ln}: {cond}")
+    assert not bad, bad
+    # the checker itself finds the pattern
+    assert _barriers_under_branches_in_ticket_loops("for (;;) { if (u == 3) { __syncthreads(); } }")
