@@ -82,6 +82,7 @@ struct Lf2Args {
     float *resid;
     uint32_t *fail, *dbg, *done;
     uint32_t tag, skip;
+    float t, inc;  // the key's state as this workgroup's scan read it (the state is updated only after every chunk)
 };
 
 struct Lf2Dec {
@@ -147,8 +148,7 @@ __device__ __forceinline__ void lf2_decide(Lf2Lds &L, Lf2Dec &D, uint32_t (&h)[4
     uint32_t sw = 0, bad = 0;
     D.ok = true;
     if (tid < A.tl) L.tail[tid] = *gp(A.src + (size_t)A.nb * 16 + tid);  // (in LDS: thread 0 sums them in order)
-    const float t0 = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(&A.cp->t)));
-    const float i0 = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(&A.cp->inc)));
+    const float t0 = A.t, i0 = A.inc;
     for (uint32_t h0 = 0; h0 * RH * LF2_WG < nc; ++h0) {
         uint64_t x[RH];
 #pragma unroll
@@ -652,7 +652,7 @@ __device__ __forceinline__ bool lf2_ranker(Lf2Lds &L, uint32_t rk) {
 }
 
 // After the chunk loop, in the last F workgroups of the grid: role `role`.
-__device__ __forceinline__ void lf2_finish(Lf2Lds &L, const LScanArgs &A, uint32_t role) {
+__device__ __forceinline__ void lf2_finish(Lf2Lds &L, const LScanArgs &A, uint32_t role, float t, float inc) {
     const uint32_t tid = threadIdx.x;
     __syncthreads();  // every wave is out of the chunk loop: the LDS goes to the finish
     if (tid == 0) {
@@ -685,6 +685,8 @@ __device__ __forceinline__ void lf2_finish(Lf2Lds &L, const LScanArgs &A, uint32
         a.done = A.done;
         a.tag = A.tag;
         a.skip = A.skip;
+        a.t = t;
+        a.inc = inc;
     }
     __syncthreads();
     if (role == 0) LF2_STAMP_MAX(1);

@@ -148,8 +148,11 @@ union LScanLds {
 };
 static_assert(sizeof(LScanLds) <= 160 * 1024 / 8, "eight scan workgroups per CU");
 
+// Eight waves per SIMD (64 VGPRs) for the plain and error-feedback scans, whose
+// finish (tv16lf2.h) would otherwise set the register budget; the gather
+// scans keep theirs (their finish is the fill launch's).
 template <bool EF, uint32_t NW, uint32_t D, uint32_t GS>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8, 8))) tv16_lscan(LScanArgs A) {
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS ? 1 : 8, 8))) tv16_lscan(LScanArgs A) {
     __shared__ LScanLds U;
     LLds &L = U.s;
     const uint32_t tid = threadIdx.x;
@@ -172,7 +175,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8,
         for (uint32_t i = tid; i < LNBIN; i += NW * 64) st_sc1(A.whist_next + i, 0u);
     const uint32_t s = uni(tid >> 6), lane = flane(), q = lane & 3u;
     const uint32_t lane_line = s * 16 + (lane >> 2);
-    float t = 0.f;
+    float t = 0.f, inc0 = 0.f;
     uint32_t tb = 0, wlo = 0;
     for (uint32_t j = 0;; ++j) {
         const uint32_t c = blockIdx.x + j * gridDim.x;
@@ -236,6 +239,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8,
         if (STG_LF2_STAMPS && j == 0 && blockIdx.x == 0 && tid == 0) A.dbg[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
         if (j == 0) {  // the threshold, read while the chunk's first loads are in flight
             t = uni(A.state->t);
+            inc0 = uni(A.state->inc);
             if (blockIdx.x == 0 && tid == 0) {  // the finish decides with the threshold the scan used
                 st_sc1(reinterpret_cast<uint32_t *>(&A.cp->t), f2u(t));
                 st_sc1(reinterpret_cast<uint32_t *>(&A.cp->inc), f2u(A.state->inc));
@@ -322,7 +326,8 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(8,
             }
         }
     }
-    if (!STG_LSCAN_DIAG && A.fin && blockIdx.x + A.fin >= gridDim.x) lf2_finish(U.f, A, blockIdx.x + A.fin - gridDim.x);
+    if (!STG_LSCAN_DIAG && !GS && A.fin && blockIdx.x + A.fin >= gridDim.x)
+        lf2_finish(U.f, A, blockIdx.x + A.fin - gridDim.x, t, inc0);
 }
 
 // diagnostics (STG_DEBUG_NOOP): a launch whose workgroups read one word and
