@@ -61,6 +61,8 @@ struct Workspace {
     // threshold-v: the ticket's value at the next call, the last call's
     // range-descriptor tag and the descriptor block last zeroed (tile_cnt, its size)
     uint64_t tv_base = 0;
+    uint32_t tv_ng[2] = {0, 0};  // threshold-v: chunk groups the last call of each parity used
+    uint32_t tv_par = 0;
     uint32_t tv_tag = 0;
     uint32_t *tv_desc = nullptr;
     size_t tv_desc_cap = 0;
@@ -114,6 +116,9 @@ struct Workspace {
         const size_t o_crew = carve(sizeof(stg::CrewCtl) * stg::MAX_BATCH);
         const size_t o_tkc = carve(sizeof(stg::TopkCtl) * 2);
         const size_t o_tkf = carve(sizeof(uint32_t) * 2 * stg::TK2_FINE);
+        const size_t o_tkd = carve(sizeof(uint64_t) * stg::TOPK_LIST_TILES);
+        const size_t o_tku = carve(sizeof(uint32_t) * (2 * stg::TK2_UNITS + 4));
+        const size_t o_tvg = carve(sizeof(uint32_t) * (4 * stg::TV_MAXNG + 1));
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
         // control block are ordered after it (a plain hipMemset runs on the
@@ -133,6 +138,9 @@ struct Workspace {
         d.crew = reinterpret_cast<stg::CrewCtl *>(b + o_crew);
         d.tkctl = reinterpret_cast<stg::TopkCtl *>(b + o_tkc);
         d.tkfine = reinterpret_cast<uint32_t *>(b + o_tkf);
+        d.tkdesc = reinterpret_cast<uint64_t *>(b + o_tkd);
+        d.tkdone = reinterpret_cast<uint32_t *>(b + o_tku);
+        d.tvg = reinterpret_cast<uint32_t *>(b + o_tvg);
         return STG_OK;
     }
 
@@ -557,8 +565,10 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         KeyState *st;
         bool fresh;
         if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
-        // range descriptors: two words per range at tile_cnt, maxima at tile_aux
-        if ((rc = ws->ensure(1, 2 * (size_t)stg::TV_MAXG, 1))) return rc;
+        // chunk lists at sums, counts at tile_cnt, maxima at tile_aux (tv.hip);
+        // STG_TV_PASS=1: range descriptors, two words per range
+        if ((rc = ws->ensure(stg::tv_list_words(n), std::max<size_t>(2 * (size_t)stg::TV_MAXG, stg::tv_chunks(n)), 1)))
+            return rc;
         if (ws->tv_desc != ws->d.tile_cnt || ws->tv_desc_cap != ws->cap_tiles) {  // fresh memory: no stale tags
             HIP_TRY(hipMemsetAsync(ws->d.tile_cnt, 0, ws->cap_tiles * sizeof(uint32_t), s));
             HIP_TRY(hipMemsetAsync(ws->d.tile_aux, 0, ws->cap_tiles * sizeof(uint32_t), s));
@@ -568,7 +578,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         if (++ws->tv_tag == 0) ws->tv_tag = 1;
         uint32_t grid = 0;
         stg::TvLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, d_count, st, fresh, h->num_cu, ev,
-                        ws->tv_tag, ws->tv_base, &grid};
+                        ws->tv_tag, ws->tv_base, &grid, ws->tv_ng, ws->tv_par ^= 1u};
         HIP_TRY(stg::launch_tv(a, ws->d, s));
         ws->tv_base += grid;
     } else {

@@ -11,16 +11,21 @@
 // last T (KeyState.t; the band's relative half width d in KeyState.inc) fixes
 // a band [F, H) = T_prev (1 -/+ d), at most TK2_FINE ulps wide, that almost
 // always holds this call's T.  Two launches:
-//   tk2_stream  one workgroup per 32 KiB tile, no waits: the tile's superset
+//   tk2_stream  one workgroup per 32 KiB tile: the tile's superset
 //               {|x| >= F} (in index order) into region tile % 32 at an offset
 //               taken by one atomic; its count of keys >= H; every band key
 //               into the band histogram, one bin per ulp (and a coarse one per
-//               256 ulps).  One read of the bucket.
-//   tk_one      every workgroup finds T exactly from the histograms (the count
-//               above H, the coarse bins, one coarse bin's 256 ulps: T is a
-//               bin), then emission units of 16 tiles in ticket order count
-//               their supersets' (> T, == T) keys, publish them, sum the
-//               earlier units' (look-back) and write their winners in order.
+//               256 ulps).  One read of the bucket.  Its first NU workgroups,
+//               after their own tiles, finish the call (tk2_finish): once
+//               every tile's descriptor carries the call's tag, each finds T
+//               exactly from the histograms (the count above H, the coarse
+//               bins, one coarse bin's 256 ulps: T is a bin), then as one of
+//               the NU emission units (up to 16 tiles) counts its supersets'
+//               (> T, == T) keys, publishes them, sums the earlier units'
+//               (look-back) and writes its winners in order.
+//   tk_one      returns at once when every unit is done; otherwise (a band
+//               that missed, or a finish that could not run) the same pick and
+//               emission by units in ticket order.
 // A band that misses T, or a superset region that overflowed, takes the
 // select's way inside tk_one (three radix levels over the bucket, per-tile
 // counts, emission re-reading the tiles; units by sharded tickets, every
@@ -98,114 +103,6 @@ __device__ __forceinline__ Band band_of(const KeyState *st) {
 }
 
 // ---------------------------------------------------------------------------
-// the stream launch
-// ---------------------------------------------------------------------------
-struct T2Stream {
-    const float *a;
-    uint64_t m;
-    uint32_t last_mask, nt;
-    const KeyState *state;
-    TopkCtl *ctl;
-    uint32_t *fine;        // this call's band histogram (TK2_FINE words, zero)
-    uint2 *sup;            // superset regions: TK2_REG of shard_cap entries {element, bits}
-    uint32_t shard_cap;
-    uint32_t *sup_n, *sup_off;  // per tile: superset entries, offset in region tile % TK2_REG
-    uint32_t *count_out;
-    uint32_t cap;
-    bool fixed;            // tile t's superset at slot t / TK2_REG of its region (no offset atomic)
-};
-
-template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) tk2_stream(const T2Stream A) {
-    __shared__ uint32_t s_wt[TILE_U * STG_WAVES + 1];
-    __shared__ uint32_t s_off, s_hi;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, tile = blockIdx.x;
-    const Band B = band_of(A.state);
-    if (!B.ok) return;  // tk_one takes the select's way (band_ok stays 0)
-    if (tile == 0 && tid == 0) {
-        *A.count_out = A.cap;  // the band's way fills every slot; a failure in tk_one poisons it (atomicMax)
-        A.ctl->band_F = B.F;
-        A.ctl->band_H = B.H;
-        A.ctl->band_ok = 1u;
-    }
-    if (tid == 0) s_hi = 0;
-    const size_t base = (size_t)tile * TV_TILE, m = A.m;
-    float4 v[TILE_U];
-    load_tile<VEC>(A.a, m, base, A.last_mask, v);
-    uint32_t q = 0, pre[TILE_U], nhi = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < TILE_U; ++u) {
-        const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t key = mag1(f2u(comp(v[u], j)));
-            if (e + j < m && key >= B.F) {
-                q |= 1u << (u * 4 + j);
-                if (key >= B.H) {
-                    ++nhi;
-                } else {
-                    const uint32_t f = key - B.F;
-                    __hip_atomic_fetch_add(gp(&A.fine[f]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(gp(&A.ctl->coarse[coarse_word(f >> TK2_CSH)]), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-        }
-        const uint32_t c = (uint32_t)__popc((q >> (4 * u)) & 0xfu);
-        const uint32_t incl = wave_incl_scan(c);
-        pre[u] = incl - c;
-        if (lane == 63) s_wt[u * STG_WAVES + wave] = incl;
-    }
-    nhi = wave_sum(nhi);
-    __syncthreads();
-    if (lane == 0 && nhi) atomicAdd(&s_hi, nhi);
-    if (tid < 64) {  // (u, wave) offsets: one wave scans the 32 counts
-        constexpr uint32_t NW = TILE_U * STG_WAVES;
-        static_assert(NW <= 64, "one wave scans the wave counts");
-        const uint32_t x = tid < NW ? s_wt[tid] : 0u;
-        const uint32_t inc = wave_incl_scan(x);
-        if (tid < NW) s_wt[tid] = inc - x;
-        if (tid == NW - 1) s_wt[NW] = inc;
-    }
-    __syncthreads();
-    const uint32_t nsup = s_wt[TILE_U * STG_WAVES], sh = tile % TK2_REG;
-    if (tid == 0) {
-        uint32_t off = 0;
-        if (nsup && A.fixed) {  // TOPK_SUP_CAP entries of the region per tile; more: the select's way
-            off = tile / TK2_REG * TOPK_SUP_CAP;
-            if (nsup > TOPK_SUP_CAP) A.ctl->ovf = 1u;
-        } else if (nsup) {
-            off = g_add(&A.ctl->shn[sh][0], nsup);
-            if (off + nsup > A.shard_cap) A.ctl->ovf = 1u;
-        }
-        s_off = off;
-        A.sup_n[tile] = nsup;
-        A.sup_off[tile] = off;
-        if (s_hi) g_add(&A.ctl->hi[tile % TK2_HI][0], s_hi);
-    }
-    __syncthreads();
-    const uint32_t off = s_off;
-    if (!nsup || off + nsup > A.shard_cap || (A.fixed && nsup > TOPK_SUP_CAP)) return;
-    uint2 *const dst = A.sup + (size_t)sh * A.shard_cap + off;
-#pragma unroll
-    for (uint32_t u = 0; u < TILE_U; ++u) {
-        const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
-        uint32_t slot = s_wt[u * STG_WAVES + wave] + pre[u];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if ((q >> (u * 4 + j)) & 1u) dst[slot++] = make_uint2((uint32_t)(e + j), f2u(comp(v[u], j)));
-    }
-}
-
-// A key's first call ran topk.hip's launches: T (rs->prefix) seeds the hint.
-__global__ void tk2_seed(KeyState *st, const RSel *rs, uint32_t *dbg) {
-    st->t = u2f(rs->prefix);
-    st->inc = D_SEED;
-    st->init = 1;
-    atomicAdd(&dbg[39], 1u);  // a call that took the select's way
-}
-
-// ---------------------------------------------------------------------------
 // the emission launch
 // ---------------------------------------------------------------------------
 struct T1Args {
@@ -222,27 +119,56 @@ struct T1Args {
     TopkCtl *ctl, *ctl_next;
     uint32_t tag;          // >= 1
     RSel *rs;              // the select's way
-    const uint2 *sup;      // the stream launch's superset regions
+    uint2 *sup;            // the stream launch's superset regions
     uint32_t shard_cap;
-    const uint32_t *sup_n, *sup_off;
+    uint32_t *sup_n, *sup_off;
     uint32_t *tile_gt, *tile_eq;  // the select's way: counts [0, nt), prefixes [nt, 2nt), totals [2nt]
-    const uint32_t *fine;  // this call's band histogram
-    uint32_t *fine_next;   // the next call's (zeroed here)
+    uint32_t *fine;        // this call's band histogram
+    uint32_t *fine_next;   // the other parity's (the stream launch zeroes what the previous call touched)
     uint32_t *dbg;         // ws.misc: [38] calls resolved in the band, [39] calls that took the select's way
     uint32_t ut;           // tiles per emission unit (<= TK2_UT): about ER STG_WG superset entries
     bool force_miss;       // tests (STG_TK1_DEBUG=2): the select's way every call
+    bool withhold;         // tests (STG_DEBUG_TK_WITHHOLD=1): unit 0 never publishes its counts, so every
+                           // later unit's look-back runs out its bound: the failure path end to end
+    bool fixed;            // tile t's superset at slot t / TK2_REG of its region (no offset atomic)
+    // the finish inside the stream launch: its first `fin` workgroups are the
+    // emission units (0: tk_one emits); tile t's descriptor tdesc[t] = tag <<
+    // 32 | superset entries; unit u done in the stream launch: done[u] = tag
+    uint32_t fin;
+    uint64_t *tdesc;
+    uint32_t *done;
+    uint64_t *pick;        // [2] the picker's {tag << 32 | hit}, {keys > T << 32 | T}
 };
 
 constexpr uint32_t ER = 8;  // superset entries per thread per emission round
 
-struct T1Lds {
+struct T1Ldf {  // the band's way (pick and emission units)
     uint32_t s_wt[TILE_U * STG_WAVES + 1];
     uint32_t sh[STG_WAVES + 1];
     uint64_t sh64[STG_WAVES];
-    uint32_t h[2048];       // a select level's tile histogram
     uint32_t uc[TK2_UT], uo[TK2_UT], up[TK2_UT + 1], ub[TK2_UT];  // emission unit: per tile count, offset, flat start, base
     uint32_t v[16];
 };
+struct T1Lds : T1Ldf {
+    uint32_t h[2048];       // a select level's tile histogram
+};
+
+// Loads of what the stream launch wrote: plain after the kernel boundary
+// (tk_one), sc1 inside the stream launch (its finish: the writers stored sc1)
+template <bool COH>
+__device__ __forceinline__ uint32_t ldw(const uint32_t *p) {
+    if constexpr (COH) return ld_sc1(p);
+    else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ uint2 ldw(const uint2 *p) {
+    if constexpr (COH) {
+        const uint64_t w = ld_sc1(reinterpret_cast<const uint64_t *>(p));
+        return make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+    } else {
+        return *p;
+    }
+}
 
 // shard s of a phase with U units holds units s, s + 8, ...
 __device__ __forceinline__ uint32_t shard_units(uint32_t U, uint32_t s) { return U > s ? (U - s + TK1_SH - 1) / TK1_SH : 0u; }
@@ -258,18 +184,22 @@ __device__ __forceinline__ void t1_broken(const T1Args &A) {
 struct Pick {
     uint32_t T, gt;  // T; keys > T
 };
-__device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
+// (COH: inlined into the stream launch, which makes no calls -- a kernel that
+// calls a function is also given the LDS of every kernel whose variables a
+// called function might reach: tk_one's 17 KiB; tk_one calls the plain copies)
+template <bool COH>
+__device__ __forceinline__ bool pick_exact(const T1Args &A, T1Ldf &L, Pick &P) {
     const uint32_t tid = threadIdx.x;
     const TopkCtl *const C = A.ctl;
-    // plain loads: written by the stream launch (a kernel boundary), read by
-    // every workgroup -- cached in each XCD's L2, where coherent (sc1) loads of
-    // the same few lines by 512 workgroups queue at the memory side
-    const uint32_t ok = C->band_ok, ovf = C->ovf, F = C->band_F;
+    // tk_one: plain loads (written by the stream launch, a kernel boundary,
+    // read by every workgroup -- cached in each XCD's L2, where coherent loads
+    // of the same few lines by 512 workgroups queue at the memory side)
+    const uint32_t ok = ldw<COH>(&C->band_ok), ovf = ldw<COH>(&C->ovf), F = ldw<COH>(&C->band_F);
     constexpr uint32_t PER = TK2_COARSE / STG_WG;
-    uint32_t c[PER], s = 0, hi = tid < TK2_HI ? C->hi[tid][0] : 0u;
+    uint32_t c[PER], s = 0, hi = tid < TK2_HI ? ldw<COH>(&C->hi[tid][0]) : 0u;
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {  // top-down: thread tid holds coarse bins 1023 - (PER tid + j)
-        c[j] = C->coarse[coarse_word(TK2_COARSE - 1u - (PER * tid + j))];
+        c[j] = ldw<COH>(&C->coarse[coarse_word(TK2_COARSE - 1u - (PER * tid + j))]);
         s += c[j];
     }
     uint32_t th, tband;
@@ -286,8 +216,8 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
     const bool pre = t0 < A.nt && tid < std::min(A.ut, A.nt - t0);
     uint32_t pc = 0, po = 0;
     if (pre) {
-        pc = A.sup_n[t0 + tid];
-        po = A.sup_off[t0 + tid];
+        pc = ldw<COH>(&A.sup_n[t0 + tid]);
+        po = ldw<COH>(&A.sup_off[t0 + tid]);
     }
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
@@ -296,7 +226,7 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
     }
     __syncthreads();
     const uint32_t cb = L.v[2], rc = L.v[3];
-    const uint32_t f = A.fine[(cb << TK2_CSH) + (1u << TK2_CSH) - 1u - tid];  // top-down
+    const uint32_t f = ldw<COH>(&A.fine[(cb << TK2_CSH) + (1u << TK2_CSH) - 1u - tid]);  // top-down
     static_assert((1u << TK2_CSH) == STG_WG, "one fine bin per thread");
     if (pre) {  // (after the fine load is issued: its round trip overlaps theirs)
         L.uc[tid] = pc;
@@ -319,15 +249,18 @@ __device__ __noinline__ bool pick_exact(const T1Args &A, T1Lds &L, Pick &P) {
 // are taken in ticket order, so each is held by a running or finished
 // workgroup) and writes the winners at their offsets.  Returns false when a
 // wait gave up.  `pre`: the tiles' counts and offsets are in L.uc / L.uo
-// already (pick_exact loads them).
-__device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, uint32_t T, uint64_t need_eq,
-                                       bool pre) {
+// already (pick_exact loads them).  `get(T, need_eq)` supplies T once the
+// unit's first round of entries is in flight (the stream launch's finishers
+// wait for the pick there): > 0 go on, 0 skip the unit, < 0 a wait gave up.
+// Returns 1 emitted, 0 skipped, -1 a wait gave up.
+template <bool COH, class GetT>
+__device__ __forceinline__ int emit_unit(const T1Args &A, T1Ldf &L, uint32_t u, GetT get, bool pre) {
     const uint32_t tid = threadIdx.x, nt = A.nt;
     const uint32_t UT = A.ut, t0 = u * UT, nT = std::min(UT, nt - t0);
     if (!pre) {
         if (tid < nT) {
-            L.uc[tid] = A.sup_n[t0 + tid];
-            L.uo[tid] = A.sup_off[t0 + tid];
+            L.uc[tid] = ldw<COH>(&A.sup_n[t0 + tid]);
+            L.uo[tid] = ldw<COH>(&A.sup_off[t0 + tid]);
         }
         __syncthreads();
     }
@@ -344,11 +277,12 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
         if (tid == 0) L.v[11] = b ? 1u : 0u;
     }
     __syncthreads();
-    if (L.v[11]) {  // cannot happen: the stream launch wrote every tile's count and offset
-        if (tid == 0) t1_broken(A);
-        return true;
-    }
-    const uint32_t N = L.up[nT];
+    // A bad count or offset cannot follow a pick that hit (the stream launch
+    // wrote every tile's; an overflowing tile marks the call ovf, a miss).
+    // The stream launch's finishers get here before they know the pick, so
+    // the verdict waits for it.
+    const bool broken = L.v[11] != 0;
+    const uint32_t N = broken ? 0u : L.up[nT];
     // the tiles' flat starts in scalar registers: entry f's tile is the count of
     // starts (after the first) at or below f -- no branch, so a round's loads
     // are all issued before any is waited for
@@ -359,7 +293,7 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
         uint32_t j = 0;
 #pragma unroll
         for (uint32_t t = 0; t + 1 < TK2_UT; ++t) j += st1[t] <= f ? 1u : 0u;
-        return A.sup[L.ub[j] + f];
+        return ldw<COH>(&A.sup[L.ub[j] + f]);
     };
     uint2 e[ER];
     auto load_round = [&](uint32_t b0) {
@@ -369,10 +303,19 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
             e[r] = ld(std::min(f, N ? N - 1u : 0u));
         }
     };
+    if (N) load_round(0);
+    uint32_t T;
+    uint64_t need_eq;
+    const int g = get(T, need_eq);  // (uniform)
+    if (g <= 0) return g;
+    if (broken) {
+        if (tid == 0) t1_broken(A);
+        return 1;
+    }
     // counts
     uint32_t gt = 0, eq = 0;
     for (uint32_t b0 = 0; b0 < N; b0 += ER * STG_WG) {
-        load_round(b0);
+        if (b0) load_round(b0);
 #pragma unroll
         for (uint32_t r = 0; r < ER; ++r) {
             const uint32_t key = mag1(e[r].y);
@@ -386,7 +329,7 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
     (void)blk_excl_scan<STG_WAVES>(eq, L.sh, &EQ);
     TopkCtl *const C = A.ctl;
     TK1_STAMP_MAX(46);  // the last unit counted
-    if (tid == 0) st_sc1(&C->udesc[u], ((uint64_t)(GT | 0x80000000u) << 32) | EQ);
+    if (tid == 0 && !(A.withhold && u == 0)) st_sc1(&C->udesc[u], ((uint64_t)(GT | 0x80000000u) << 32) | EQ);
     // look-back: the earlier units' counts, one thread per unit
     uint64_t pg = 0, pe = 0;
     uint32_t bad = 0;
@@ -401,10 +344,10 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
         pg += (w >> 32) & 0x7fffffffu;
         pe += (uint32_t)w;
     }
-    if (__syncthreads_or((int)bad)) return false;
+    if (__syncthreads_or((int)bad)) return -1;
     TK1_STAMP_MAX(47);  // the last look-back done
     const uint64_t gt_before = blk_sum64<STG_WAVES>(pg, L.sh64), eq_before = blk_sum64<STG_WAVES>(pe, L.sh64);
-    if (!(GT || (EQ && eq_before < need_eq))) return true;
+    if (!(GT || (EQ && eq_before < need_eq))) return 1;
     // emission: > T always, == T in index order while fewer than need_eq came before
     uint64_t wbase = gt_before + std::min(eq_before, need_eq), ebase = eq_before;
     for (uint32_t b0 = 0; b0 < N; b0 += ER * STG_WG) {
@@ -436,7 +379,292 @@ __device__ __noinline__ bool emit_unit(const T1Args &A, T1Lds &L, uint32_t u, ui
         wbase += tw;
         ebase += te;
     }
-    return true;
+    return 1;
+}
+
+__device__ __noinline__ bool pick_exact_call(const T1Args &A, T1Ldf &L, Pick &P) { return pick_exact<false>(A, L, P); }
+// false: a wait gave up
+__device__ __noinline__ bool emit_unit_call(const T1Args &A, T1Ldf &L, uint32_t u, uint32_t T, uint64_t need_eq) {
+    auto known = [&](uint32_t &t, uint64_t &ne) -> int { t = T; ne = need_eq; return 1; };
+    return emit_unit<false>(A, L, u, known, true) >= 0;
+}
+
+// ---------------------------------------------------------------------------
+// the stream launch
+// ---------------------------------------------------------------------------
+
+#ifndef STG_TK2_SUP_PLAIN
+#define STG_TK2_SUP_PLAIN 0  // A/B diagnostics: plain superset stores (valid only with STG_TK2_FIN=0)
+#endif
+#ifndef STG_TK1_SKIPALL
+#define STG_TK1_SKIPALL 0  // A/B diagnostics: tk_one returns at once whenever the stream launch finishes
+#endif
+#ifndef STG_TK2_NOFIN
+#define STG_TK2_NOFIN 0  // A/B diagnostics: no finish code in the stream launch (run with STG_TK2_FIN=0)
+#endif
+#ifndef STG_TK2_ZERO_LATE
+#define STG_TK2_ZERO_LATE 0  // A/B diagnostics: the previous call's zeroing after the tile, not before
+#endif
+
+// The finish inside the stream launch, by emission unit u (one of its first
+// A.fin workgroups, each after its own tile): wait for every tile's
+// descriptor, pick T from the histograms, emit the unit (look-back among the
+// finishing workgroups, all resident: the grid's last ones), then done[u].
+// Any wait that gives up, and a band that missed, leaves done[u] unset: tk_one
+// then runs as the finish (the select's way on a miss).
+__device__ __forceinline__ void tk2_finish(const T1Args &A, T1Ldf &L, uint32_t u) {
+    const uint32_t tid = threadIdx.x, nt = A.nt;
+    const uint32_t t0 = u * A.ut, nT = std::min(A.ut, nt - t0);
+    uint64_t st = 0;
+    auto gave_up = [&]() {
+        if (tid == 0) atomicAdd(&A.dbg[59], 1u);
+    };
+    int r;
+    if (u == 0) {
+        // The picker (the first workgroup): every tile's descriptor, rereading
+        // only the ones not yet seen, then T from the histograms, published
+        // as {tag << 32 | hit} after {keys > T << 32 | T}.  The other
+        // finishers poll that one word with one lane: every finisher reading
+        // the histograms itself put ~100 lines x NU coherent loads in the
+        // memory-side queues.
+        constexpr uint32_t PR = 8, PT = TOPK_LIST_TILES / STG_WG;
+        static_assert(PT <= 32, "a seen bit per tile");
+        uint32_t seen = 0;
+        for (uint32_t sp = 0;; ++sp) {
+            uint32_t miss = 0;
+            for (uint32_t g = 0; g < PT && g * STG_WG < nt; g += PR) {  // uniform
+                uint64_t w[PR];
+#pragma unroll
+                for (uint32_t q = 0; q < PR; ++q) {
+                    const uint32_t t = tid + (g + q) * STG_WG;
+                    w[q] = t < nt && !((seen >> (g + q)) & 1u) ? ld_sc1(&A.tdesc[t]) : (uint64_t)A.tag << 32;
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < PR; ++q) {
+                    if ((uint32_t)(w[q] >> 32) == A.tag) seen |= 1u << (g + q);
+                    else miss = 1;
+                }
+            }
+            if (!__syncthreads_or((int)miss)) break;
+            const bool ex = spin_expired(sp, st);
+            if (__syncthreads_or((int)(tid == 0 && ex))) {  // (uniform) tk_one finishes
+                gave_up();
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        TK1_STAMP(49);  // the picker saw every tile
+        if (tid == 0) L.v[9] = 0;
+        __syncthreads();
+        Pick P;
+        const bool hit = !A.force_miss && pick_exact<true>(A, L, P);
+        if (tid == 0) {
+            if (hit) {  // the next call's hint (tk_one's rule); no finisher reads the state
+                const float Tp = A.state->t, d = A.state->inc, Tf = u2f(P.T);
+                A.state->t = Tf;
+                A.state->inc = fabsf(Tf - Tp) < 0.25f * d * Tp ? fmaxf(0.75f * d, D_MIN) : fminf(d, D_MAX);
+                atomicAdd(&A.dbg[38], 1u);
+                atomicAdd(&A.dbg[49], 1u);  // ... finished inside the stream launch
+                st_sc1(&A.pick[1], (uint64_t)P.gt << 32 | P.T);
+                vm_drain();
+            } else {
+                atomicAdd(&A.dbg[58], 1u);
+            }
+            st_sc1(&A.pick[0], (uint64_t)A.tag << 32 | (hit ? 1u : 0u));
+        }
+        TK1_STAMP(42);  // the pick published
+        if (!hit) return;  // (uniform) tk_one: the select's way
+        auto known = [&](uint32_t &t, uint64_t &ne) -> int {
+            t = P.T;
+            ne = (uint64_t)A.k - P.gt;
+            return 1;
+        };
+        r = emit_unit<true>(A, L, 0, known, true);  // (pick_exact loaded unit 0's tiles)
+    } else {
+        // the unit's own tiles described, then its supersets' first round
+        // loaded while the pick is awaited (emit_unit calls `wait` with them
+        // in flight)
+        for (uint32_t sp = 0;; ++sp) {
+            const bool miss = tid < nT && (uint32_t)(ld_sc1(&A.tdesc[t0 + tid]) >> 32) != A.tag;
+            if (!__syncthreads_or((int)miss)) break;
+            const bool ex = spin_expired(sp, st);
+            if (__syncthreads_or((int)(tid == 0 && ex))) {  // (uniform) tk_one finishes
+                gave_up();
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        auto wait = [&](uint32_t &t, uint64_t &ne) -> int {
+            if (tid == 0) {
+                uint64_t w = ld_sc1(&A.pick[0]), st2 = 0;
+                uint32_t ok = 1;
+                for (uint32_t sp = 0; (uint32_t)(w >> 32) != A.tag; ++sp) {
+                    __builtin_amdgcn_s_sleep(4);
+                    w = ld_sc1(&A.pick[0]);
+                    if (spin_expired(sp, st2)) { ok = 2; break; }
+                }
+                if (ok == 1 && !(w & 1u)) ok = 0;
+                if (ok == 1) {
+                    const uint64_t x = ld_sc1(&A.pick[1]);
+                    L.v[5] = (uint32_t)x;
+                    L.v[6] = (uint32_t)(x >> 32);
+                }
+                L.v[8] = ok;
+            }
+            __syncthreads();
+            const uint32_t ok = L.v[8];
+            t = L.v[5];
+            ne = (uint64_t)A.k - L.v[6];
+            __syncthreads();
+            TK1_STAMP_MAX(43);  // the last finisher has the pick
+            if (ok == 2) gave_up();
+            return ok == 1 ? 1 : 0;  // a miss or a wait that gave up: tk_one finishes
+        };
+        r = emit_unit<true>(A, L, u, wait, false);
+    }
+    if (r < 0) {
+        if (tid == 0) {
+            g_or(A.fail, FAIL_SPIN_TIMEOUT);
+            __hip_atomic_fetch_max(gp(A.count_out), POISON_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    if (r == 0) return;
+    TK1_STAMP_MAX(50);  // the last unit emitted
+    vm_drain();
+    __syncthreads();
+    if (tid == 0) {
+        st_sc1(&A.done[u], A.tag);
+        atomicAdd(&A.dbg[56], 1u);  // units finished inside the stream launch
+    }
+}
+
+// One workgroup per tile.  Before its tile, each zeroes its share of the
+// previous hinted call's control block (from its second line on) and of the
+// fine bins that call's band touched (ctl_next keeps the band: [0, H - F)).
+template <bool VEC>
+__global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(7, 8))) tk2_stream(const T1Args A) {
+    __shared__ T1Ldf L;
+    __shared__ uint32_t s_off, s_hi;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, tile = blockIdx.x, nt = A.nt;
+    const Band B = band_of(A.state);
+    const size_t base = (size_t)tile * TV_TILE, m = A.m;
+    float4 v[TILE_U];
+    if (B.ok) load_tile<VEC>(A.a, m, base, A.last_mask, v);
+    auto zero_prev = [&]() {
+        const TopkCtl *const cn = A.ctl_next;
+        const uint32_t span = cn->band_ok ? std::min(cn->band_H - cn->band_F, TK2_FINE) : 0u;
+        constexpr uint32_t CW = (uint32_t)((sizeof(TopkCtl) - 4u * TK1_LINE) / 16u);
+        uint4 *const c4 = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(A.ctl_next) + 4u * TK1_LINE);
+        uint4 *const f4 = reinterpret_cast<uint4 *>(A.fine_next);
+        for (uint32_t i = tile * STG_WG + tid, n = CW + (span + 3u) / 4u; i < n; i += nt * STG_WG) {
+            if (i < CW) c4[i] = make_uint4(0u, 0u, 0u, 0u);
+            else f4[i - CW] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    if (!STG_TK2_ZERO_LATE || !B.ok) zero_prev();
+    if (!B.ok) return;  // tk_one takes the select's way (band_ok stays 0)
+    if (tile == 0) TK1_STAMP(40);  // the stream launch's first workgroup starts
+    TopkCtl *const C = A.ctl;
+    if (tile == 0 && tid == 0) {
+        st_sc1(A.count_out, A.cap);  // the band's way fills every slot; a failure poisons it (atomicMax)
+        st_sc1(&C->band_F, B.F);
+        st_sc1(&C->band_H, B.H);
+        st_sc1(&C->band_ok, 1u);
+    }
+    if (tid == 0) s_hi = 0;
+    uint32_t q = 0, pre[TILE_U], nhi = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < TILE_U; ++u) {
+        const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t key = mag1(f2u(comp(v[u], j)));
+            if (e + j < m && key >= B.F) {
+                q |= 1u << (u * 4 + j);
+                if (key >= B.H) {
+                    ++nhi;
+                } else {
+                    const uint32_t f = key - B.F;
+                    __hip_atomic_fetch_add(gp(&A.fine[f]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_add(gp(&C->coarse[coarse_word(f >> TK2_CSH)]), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+        }
+        const uint32_t c = (uint32_t)__popc((q >> (4 * u)) & 0xfu);
+        const uint32_t incl = wave_incl_scan(c);
+        pre[u] = incl - c;
+        if (lane == 63) L.s_wt[u * STG_WAVES + wave] = incl;
+    }
+    nhi = wave_sum(nhi);
+    __syncthreads();
+    if (lane == 0 && nhi) atomicAdd(&s_hi, nhi);
+    if (tid < 64) {  // (u, wave) offsets: one wave scans the 32 counts
+        constexpr uint32_t NW = TILE_U * STG_WAVES;
+        static_assert(NW <= 64, "one wave scans the wave counts");
+        const uint32_t x = tid < NW ? L.s_wt[tid] : 0u;
+        const uint32_t inc = wave_incl_scan(x);
+        if (tid < NW) L.s_wt[tid] = inc - x;
+        if (tid == NW - 1) L.s_wt[NW] = inc;
+    }
+    __syncthreads();
+    const uint32_t nsup = L.s_wt[TILE_U * STG_WAVES], sh = tile % TK2_REG;
+    // sc1 stores throughout: the finishing workgroups of this launch read them
+    if (tid == 0) {
+        uint32_t off = 0;
+        if (nsup && A.fixed) {  // TOPK_SUP_CAP entries of the region per tile; more: the select's way
+            off = tile / TK2_REG * TOPK_SUP_CAP;
+            if (nsup > TOPK_SUP_CAP) st_sc1(&C->ovf, 1u);
+        } else if (nsup) {
+            off = g_add(&C->shn[sh][0], nsup);
+            if (off + nsup > A.shard_cap) st_sc1(&C->ovf, 1u);
+        }
+        s_off = off;
+        st_sc1(&A.sup_n[tile], nsup);
+        st_sc1(&A.sup_off[tile], off);
+        if (s_hi) g_add(&C->hi[tile % TK2_HI][0], s_hi);
+    }
+    __syncthreads();
+    const uint32_t off = s_off;
+    if (nsup && off + nsup <= A.shard_cap && !(A.fixed && nsup > TOPK_SUP_CAP)) {
+        uint64_t *const dst = reinterpret_cast<uint64_t *>(A.sup) + (size_t)sh * A.shard_cap + off;
+#pragma unroll
+        for (uint32_t u = 0; u < TILE_U; ++u) {
+            const size_t e = base + 4 * ((size_t)u * STG_WG + tid);
+            uint32_t slot = L.s_wt[u * STG_WAVES + wave] + pre[u];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((q >> (u * 4 + j)) & 1u) {
+                    const uint64_t w = (uint64_t)f2u(comp(v[u], j)) << 32 | (uint32_t)(e + j);
+                    if (STG_TK2_SUP_PLAIN) dst[slot++] = w;
+                    else st_sc1(&dst[slot++], w);
+                }
+        }
+    }
+    if (STG_TK2_ZERO_LATE) zero_prev();
+    if (!A.fin) return;
+    // the tile's descriptor once its stores and atomics are complete
+    vm_drain();
+    __syncthreads();
+    if (tid == 0) st_sc1(&A.tdesc[tile], (uint64_t)A.tag << 32 | nsup);
+    TK1_STAMP_MAX(41);  // the last tile described
+    if (STG_TK2_NOFIN || tile >= A.fin) return;
+    // The finishers are the grid's FIRST NU workgroups: resident from the
+    // start, they wait (polling lightly) while the other tiles stream, and the
+    // chain starts the moment the last tile lands.  (The last NU, dispatched
+    // last, started it a tile's lifetime late.)  Inlined with everything it
+    // calls: the argument block's fields stay scalar loads; a copy of the
+    // block, or a call taking it, puts it in memory.
+    tk2_finish(A, L, tile);
+}
+
+// A key's first call ran topk.hip's launches: T (rs->prefix) seeds the hint.
+__global__ void tk2_seed(KeyState *st, const RSel *rs, uint32_t *dbg) {
+    st->t = u2f(rs->prefix);
+    st->inc = D_SEED;
+    st->init = 1;
+    atomicAdd(&dbg[39], 1u);  // a call that took the select's way
 }
 
 // A select level's histogram over one tile (the keys under the prefix).
@@ -597,23 +825,31 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     // reference to the kernel's argument block would be copied to scratch)
     __shared__ T1Args A;
     const uint32_t tid = threadIdx.x;
-    if (tid == 0) A = Ak;
+    if (Ak.fin) {  // the stream launch finished every emission unit (read before the argument copy)
+        uint32_t miss = 0;
+        // (plain loads: written by the stream launch, a kernel boundary; sc1
+        // loads of the same few lines by every workgroup queue at the memory side)
+        if (STG_TK1_SKIPALL) return;
+        for (uint32_t i = tid; i < Ak.fin; i += STG_WG) miss |= Ak.done[i] != Ak.tag ? 1u : 0u;
+        if (!__syncthreads_or((int)miss)) return;
+        if (tid == 0) atomicAdd(&Ak.dbg[57], 1u);  // workgroups of tk_one that run after all
+    }
+    // the argument block into LDS field by field: `A = Ak` compiled to a private
+    // copy of the whole block, stored to scratch by every thread of every
+    // workgroup before anything else (~10 MB a launch, ~15 us)
+    if (tid == 0) {
+        A.a = Ak.a; A.m = Ak.m; A.zeros = Ak.zeros; A.last_mask = Ak.last_mask; A.nt = Ak.nt; A.k = Ak.k;
+        A.cap = Ak.cap; A.idx_offset = Ak.idx_offset; A.bug_compat = Ak.bug_compat; A.idx = Ak.idx; A.val = Ak.val;
+        A.count_out = Ak.count_out; A.fail = Ak.fail; A.state = Ak.state; A.ctl = Ak.ctl; A.ctl_next = Ak.ctl_next;
+        A.tag = Ak.tag; A.rs = Ak.rs; A.sup = Ak.sup; A.shard_cap = Ak.shard_cap; A.sup_n = Ak.sup_n;
+        A.sup_off = Ak.sup_off; A.tile_gt = Ak.tile_gt; A.tile_eq = Ak.tile_eq; A.fine = Ak.fine;
+        A.fine_next = Ak.fine_next; A.dbg = Ak.dbg; A.ut = Ak.ut; A.force_miss = Ak.force_miss;
+        A.withhold = Ak.withhold; A.fixed = Ak.fixed; A.fin = Ak.fin; A.tdesc = Ak.tdesc; A.done = Ak.done;
+        A.pick = Ak.pick;
+    }
     __syncthreads();
     TopkCtl *const C = A.ctl;
     if (blockIdx.x == 0) TK1_STAMP(40);
-    // the next call's control block and band histogram, zeroed in shares
-    // (this call never touches them) with plain stores at the workgroup's end:
-    // vmcnt counts stores with loads, in order, so stores issued first would
-    // hold this workgroup's later loads (the next call's launches see them
-    // after this kernel's end)
-    auto zero_next = [&]() {
-        constexpr uint32_t CW = (uint32_t)(sizeof(TopkCtl) / 16), FW = TK2_FINE / 4u;
-        uint4 *const c4 = reinterpret_cast<uint4 *>(A.ctl_next), *const f4 = reinterpret_cast<uint4 *>(A.fine_next);
-        for (uint32_t i = blockIdx.x * STG_WG + tid; i < CW + FW; i += gridDim.x * STG_WG) {
-            if (i < CW) c4[i] = make_uint4(0u, 0u, 0u, 0u);
-            else f4[i - CW] = make_uint4(0u, 0u, 0u, 0u);
-        }
-    };
     const uint32_t home = blockIdx.x % TK1_SH;
     auto poison = [&]() {
         if (tid == 0) {
@@ -628,7 +864,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     // round trip overlaps the pick's loads
     const uint32_t NU = (A.nt + A.ut - 1u) / A.ut;
     if (tid == 0) L.v[9] = blockIdx.x < NU ? g_add(&C->utk[0], 1u) : NU;
-    const bool hit = !A.force_miss && pick_exact(A, L, P);
+    const bool hit = !A.force_miss && pick_exact_call(A, L, P);
     if (blockIdx.x == 0) TK1_STAMP(42);  // workgroup 0: pick done
     TK1_STAMP_MAX(43);                   // every workgroup's pick done
     if (hit) {
@@ -644,11 +880,10 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         __syncthreads();
         if (u < NU) {
             TK1_STAMP_MAX(48);  // the last unit taken
-            if (!emit_unit(A, L, u, P.T, need_eq, true)) { poison(); zero_next(); return; }
+            if (!emit_unit_call(A, L, u, P.T, need_eq)) { poison(); return; }
             TK1_STAMP_MAX(44);  // the last unit done
         }
         TK1_STAMP_MAX(45);      // the last workgroup out
-        zero_next();
         return;
     }
     // wait for the single-unit phase p's flag (one lane polls, sparsely)
@@ -738,7 +973,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     const uint32_t seq[4] = {M_H1, M_H2, M_H3, M_CNT};
     for (uint32_t i = 0; i < 4; ++i) {
         run_multi(seq[i], 0, 0);
-        if (!wait_flag(seq[i] + 1u)) { poison(); zero_next(); return; }
+        if (!wait_flag(seq[i] + 1u)) { poison(); return; }
     }
     const uint32_t T = ld_sc1(&C->res_T);
     const uint64_t tgt = ld_sc1(&A.tile_gt[2 * A.nt]), teq = ld_sc1(&A.tile_eq[2 * A.nt]);
@@ -752,7 +987,6 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         }
     }
     run_multi(P_EMIT, T, need_eq);
-    zero_next();
 }
 
 }  // namespace
@@ -778,8 +1012,8 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
         return hipGetLastError();
     }
     // The control block and band histogram alternate by the tag's parity: each
-    // tk_one zeroes the other parity's copies for the next hinted call.  So the
-    // tag moves only here, where tk_one runs, and always to the other parity
+    // stream launch zeroes what the previous hinted call used of the other
+    // parity's copies.  So the tag moves only here, and always to the other parity
     // (0 is never a tag: 0xffffffff is followed by 2).  A launch error leaves
     // both copies in an unknown state; they are zeroed on the stream.
     const uint32_t tag = *tagp + 1u == 0u ? 2u : *tagp + 1u;
@@ -803,11 +1037,6 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     uint32_t *const sup_n = ws.tile_cnt + 2 * (size_t)nt + 1, *const sup_off = ws.tile_aux + 2 * (size_t)nt + 1;
     uint2 *const sup = reinterpret_cast<uint2 *>(ws.sums);
     const bool vec = (reinterpret_cast<uintptr_t>(a.src) & 15u) == 0;
-    if (a.ev) (void)hipEventRecord(a.ev[0], s);
-    T2Stream S{a.src, m, last_mask, nt, state, ctl, fine, sup, shard_cap, sup_n, sup_off, a.count_out, a.cap, fixed};
-    if (vec) tk2_stream<true><<<nt, STG_WG, 0, s>>>(S);
-    else tk2_stream<false><<<nt, STG_WG, 0, s>>>(S);
-    if (a.ev) (void)hipEventRecord(a.ev[1], s);
     T1Args A{};
     A.a = a.src;
     A.m = m;
@@ -843,10 +1072,30 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     A.ut = std::max(1u, std::min(A.ut, TK2_UT));
     A.fine_next = ws.tkfine + (size_t)((tag + 1u) & 1u) * TK2_FINE;
     A.dbg = ws.misc;
-    // every emission unit has a workgroup of its own (NU <= TK2_UNITS)
-    const uint32_t G = std::max<uint32_t>(std::min<uint32_t>(nt, (uint32_t)a.num_cu * 2u), (nt + A.ut - 1u) / A.ut);
+    A.fixed = fixed;
+    // the finish inside the stream launch: its first NU workgroups, one per
+    // emission unit, when that leaves most of the grid to the tiles
+    // (off by default: measured 26.5 / 37.5 us per shipped / exact C2 call
+    // against 24.4 / 35.0 with tk_one finishing; STG_TK2_FIN=1 turns it on)
+    static const bool fin_ok = getenv("STG_TK2_FIN") && atoi(getenv("STG_TK2_FIN")) == 1;
+    const uint32_t NU = (nt + A.ut - 1u) / A.ut;
+    A.fin = fin_ok && nt >= 2u * NU ? NU : 0u;
+    A.tdesc = ws.tkdesc;
+    A.done = ws.tkdone;
+    A.pick = reinterpret_cast<uint64_t *>(ws.tkdone + 2 * TK2_UNITS);
     static const int dbg_mode = getenv("STG_TK1_DEBUG") ? atoi(getenv("STG_TK1_DEBUG")) : 0;
     A.force_miss = dbg_mode == 2;
+    static const bool withhold = getenv("STG_DEBUG_TK_WITHHOLD") && atoi(getenv("STG_DEBUG_TK_WITHHOLD")) == 1;
+    A.withhold = withhold;
+    if (a.ev) (void)hipEventRecord(a.ev[0], s);
+    if (vec) tk2_stream<true><<<nt, STG_WG, 0, s>>>(A);
+    else tk2_stream<false><<<nt, STG_WG, 0, s>>>(A);
+    if (a.ev) (void)hipEventRecord(a.ev[1], s);
+    // every emission unit has a workgroup of its own (NU <= TK2_UNITS).  (A
+    // grid of just the NU units, for a cheaper idle launch behind the stream
+    // launch's finish, broke the select's way on a miss: FAIL_SELECT at 17
+    // workgroups, tests/test_gpu_alt_paths.py)
+    const uint32_t G = std::max<uint32_t>(std::min<uint32_t>(nt, (uint32_t)a.num_cu * 2u), NU);
     if (vec) tk_one<true><<<G, STG_WG, 0, s>>>(A);
     else tk_one<false><<<G, STG_WG, 0, s>>>(A);
     if (a.ev) (void)hipEventRecord(a.ev[2], s);

@@ -19,6 +19,7 @@ constexpr uint32_t TOPK_LIST_CAP = 4096;     // top-k: keys of T's level-2 bin l
 constexpr uint32_t TOPK_LIST_TILES = 8192;   // ... when the bucket has at most this many tiles (64 Mi floats)
 constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
 constexpr uint32_t TV_SCAP = 4096;           // threshold-v qualifiers listed per range (32 KiB of LDS)
+constexpr uint32_t TV_MAXNG = 16384;         // threshold-v chunk groups (32 chunks of 32 KiB) per call at most
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 constexpr uint32_t RS_SHARDS = 8;            // histogram copies: workgroup w adds into shard w % RS_SHARDS
@@ -125,12 +126,16 @@ constexpr uint32_t TK2_REG = 32;                      // superset regions (tile 
 constexpr uint32_t TK2_UT = STG_TK2_UT;               // tiles per emission unit (at most)
 constexpr uint32_t TK2_UNITS = TOPK_LIST_TILES / TK2_UT;
 struct alignas(128) TopkCtl {
+    // the stream launch's band [F, H): the next call's stream launch zeroes
+    // the fine bins [0, H - F) it touched and every line after this one
+    uint32_t band_F, band_H, band_ok;
+    uint32_t bpad[TK1_LINE - 3];
     uint32_t tk[TK1_NPH][TK1_SH][TK1_LINE];    // tickets per phase and shard
     uint32_t done[TK1_NPH][TK1_SH][TK1_LINE];  // units done per phase and shard
     uint32_t sdone[TK1_NPH][TK1_LINE];         // shards done per phase
     uint32_t flag[TK1_NPH];                    // = the call tag once single-unit phase p is done
-    uint32_t band_F, band_H, band_ok, ovf, res_T;  // the stream launch's band [F, H); a superset region overflowed
-    uint32_t pad[TK1_LINE - TK1_NPH - 5];
+    uint32_t ovf, res_T;                       // a superset region overflowed; the select's T
+    uint32_t pad[TK1_LINE - TK1_NPH - 2];
     uint32_t utk[TK1_LINE];                    // emission units taken
     uint32_t hi[TK2_HI][TK1_LINE];             // keys >= H, by tile % TK2_HI
     uint32_t shn[TK2_REG][TK1_LINE];           // superset entries placed in region tile % TK2_REG
@@ -142,6 +147,9 @@ struct DevWS {
     FillCtl *ctl;
     TopkCtl *tkctl;      // [2]
     uint32_t *tkfine;    // [2][TK2_FINE] band histograms by call parity, zero between calls
+    uint64_t *tkdesc;    // [TOPK_LIST_TILES] stream tile t: call tag << 32 | superset entries
+    uint32_t *tkdone;    // [2][TK2_UNITS] unit u finished in the stream launch / its tiles all described: = the call tag
+    uint32_t *tvg;       // [2 parities][sum, max][TV_MAXNG] threshold-v chunk-group counts and maxima, + the call's t
     CrewCtl *crew;       // MAX_BATCH slots
     ChunkDesc *desc;     // thresholdv16 chunk descriptors (grown per launch, zeroed)
     CallParams *cp;
@@ -316,8 +324,12 @@ struct TvLaunch {
     uint32_t tag;          // call tag (>= 1) of the range descriptors at ws.tile_cnt (2 words per range)
     uint64_t ticket_base;  // ws.tv_ticket's value when this call starts
     uint32_t *grid_out;    // receives the launch's range count (the ticket advances by it)
+    uint32_t *tv_ng;       // [2]: the chunk groups the last call of each parity used (host memory)
+    uint32_t par;          // this call's parity (alternates per call): group sums it accumulates into
 };
 hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s);
+uint32_t tv_chunks(size_t n);      // threshold-v chunks (32 KiB) of an n-element bucket
+uint32_t tv_list_words(size_t n);  // ... their qualifier lists, in 32-bit words (ws.sums)
 
 struct TopkLaunch {
     const float *src;

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <vector>
 
@@ -63,22 +64,31 @@ __global__ void __launch_bounds__(WG) k_chunks(const float4 *__restrict__ src, s
     if (c == 12345) out[0] = c;
 }
 
-template <int WG>
+template <int WG, bool NT = false>
 __global__ void __launch_bounds__(WG) k_onepass(const float4 *__restrict__ src, size_t n4, unsigned *out) {
     // one float4 x 8 per thread, grid = n4 / (WG*8): the v1 scan shape
     const size_t i = (size_t)blockIdx.x * WG * 8 + threadIdx.x;
     float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = src[min(i + (size_t)u * WG, n4 - 1)];
+    for (int u = 0; u < 8; ++u) {
+        const size_t j = min(i + (size_t)u * WG, n4 - 1);
+        if (NT) {
+            const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(src + j));
+            v[u] = make_float4(t.x, t.y, t.z, t.w);
+        } else {
+            v[u] = src[j];
+        }
+    }
     unsigned c = 0;
 #pragma unroll
     for (int u = 0; u < 8; ++u) c += (v[u].x + v[u].y + v[u].z + v[u].w) > 1e30f;
-    if (c == 12345) out[0] = c;
+    if (c == (unsigned)n4 + 7u) out[0] = c;  // (not provably false: the loads stay)
 }
 
-int main() {
-    const size_t n = 16u << 20, n4 = n / 4;
-    const int NB = 16;
+int main(int argc, char **argv) {
+    const size_t mib = argc > 1 ? (size_t)atoi(argv[1]) : 64;  // bucket size (MiB), rotating through >= 1 GiB
+    const size_t n = mib << 18, n4 = n / 4;
+    const int NB = (int)std::max<size_t>(2, 1024 / mib);
     std::vector<float *> bufs(NB);
     for (auto &b : bufs) { CK(hipMalloc(&b, n * 4)); CK(hipMemset(b, 0, n * 4)); }
     unsigned *out, *ctr;
@@ -110,6 +120,9 @@ int main() {
     char nm[128];
     run("onepass WG256 U8 (v1 scan)", [&](int, float *b) {
         k_onepass<256><<<(unsigned)(n4 / 2048), 256>>>((const float4 *)b, n4, out);
+    });
+    run("onepass WG256 U8 nt", [&](int, float *b) {
+        k_onepass<256, true><<<(unsigned)(n4 / 2048), 256>>>((const float4 *)b, n4, out);
     });
 #define STATIC(WG, U, NT, PER)                                                                             \
     snprintf(nm, sizeof nm, "static WG%d U%d nt%d x%d/CU", WG, U, (int)NT, PER);                          \
