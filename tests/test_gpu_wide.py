@@ -80,3 +80,58 @@ def test_bucket_past_2p20_lines(gpu, oracle):
     print("regimes", regimes, "us", [round(t, 1) for t in times], "wide", w[52:56], "paths", w[56:60])
     assert "A" in regimes[:6] and "B" in regimes[:6], regimes
     assert w[59] == 0 and w[54] == 0 and w[55] == 0, w[48:64]
+
+
+def _zero_run(gpu, oracle):
+    """A converged 64 MiB key, then a bucket in which only 2,000 of its
+    1,048,576 lines are non-zero -- fewer than the M lines regime B fills, so
+    the cut falls inside a run of a million equal (zero) line sums."""
+    import torch
+    from stellatrain_amd import ThresholdvCompressor16, merge_numel
+    n = 16 << 20
+    comp = ThresholdvCompressor16()
+    ho = oracle.tv16_new()
+    k = merge_numel(n, 0.99)
+    idx = torch.zeros(k, dtype=torch.int32, device=gpu)
+    val = torch.zeros(k, dtype=torch.float32, device=gpu)
+    rng = np.random.default_rng(9500)
+    keep = np.zeros(n // 16, dtype=bool)
+    keep[rng.choice(n // 16, 2000, replace=False)] = True
+    us = []
+    try:
+        for c in range(5):
+            x = oracle.synth(n, 9500 + c)
+            if c == 4:
+                x = (x.reshape(-1, 16) * keep[:, None]).reshape(-1).astype(np.float32)
+            d = torch.from_numpy(x).to(gpu)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            cnt = comp.compress("z@weight", d, k, idx, val)
+            e1.record()
+            torch.cuda.synchronize()
+            us.append(round(e0.elapsed_time(e1) * 1e3, 1))
+            co, io, vo = oracle.tv16_compress(ho, "z@weight", x, k)
+            assert cnt == co, (c, cnt, co)
+            assert_same_stream(idx.cpu().numpy().view(np.uint32), val.cpu().numpy(), io, vo, co)
+            assert np.float32(comp.state("z@weight")[0]).view(np.uint32) == \
+                np.float32(oracle.tv16_state(ho, "z@weight")[0]).view(np.uint32)
+        comp.check_device()
+        w = _words(comp, torch.cuda.current_stream(gpu))
+    finally:
+        oracle.tv16_free(ho)
+    print("zero-run tie: us", us, "wide", w[52:56], "paths", w[56:60])
+    return us, w
+
+
+def test_zero_run_tie_64mib(gpu, oracle):
+    """The zero-run tie at the cut, bit-exact against the oracle (order,
+    values, count, threshold)."""
+    _zero_run(gpu, oracle)
+
+
+@pytest.mark.xfail(strict=True, reason="round 5: a run of ~10^6 equal sums at the cut still takes the literal heap "
+                                       "(debug word 55 / 59); DESIGN.md section 6")
+def test_zero_run_tie_no_literal_heap(gpu, oracle):
+    us, w = _zero_run(gpu, oracle)
+    assert w[55] == 0 and w[59] == 0, w[48:64]
