@@ -44,7 +44,10 @@ namespace {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 
-constexpr uint32_t TWG = 1024;       // threads per workgroup (16 waves)
+#ifndef STG_TV_TWG
+#define STG_TV_TWG 1024
+#endif
+constexpr uint32_t TWG = STG_TV_TWG;  // threads per workgroup (16 waves)
 constexpr uint32_t TNW = TWG / 64;
 #ifndef STG_TV_WPC
 #define STG_TV_WPC 1  // workgroups per CU (1 with 6 loads in flight per lane: 52.3 us at C3; 2 with 4: 55.6)
@@ -53,7 +56,7 @@ constexpr uint32_t TNW = TWG / 64;
 #define STG_TV_SCAN_D 6
 #endif
 constexpr uint32_t SCAN_D = STG_TV_SCAN_D;  // float4 loads in flight per lane
-constexpr uint32_t LCAP = TV_SCAP;   // qualifiers listed in LDS per range
+constexpr uint32_t LCAP = TV_SCAP * TWG / 1024u;  // qualifiers listed in LDS per range
 
 __global__ void tv_init_state(KeyState *st, const RSel *rs) {
     st->t = u2f(rs->prefix);
@@ -227,15 +230,23 @@ __global__ void __launch_bounds__(TWG, 8) tv_pass(TvArgs a) {
     // the ranges finish streaming together)
     uint64_t Pl = 0;
     bool gave_up = false;
-    if (tid < r) {
-        uint64_t d = ld_sc1(&a.desc[tid]);
-        uint64_t st = 0;
+    constexpr uint32_t LB = (TV_MAXG + TWG - 1) / TWG;  // earlier ranges per thread, all loaded at once
+    uint64_t dl[LB];
+#pragma unroll
+    for (uint32_t q = 0; q < LB; ++q) {
+        const uint32_t i = tid + q * TWG;
+        dl[q] = i < r ? ld_sc1(&a.desc[i]) : (uint64_t)a.tag << 32;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < LB; ++q) {
+        const uint32_t i = tid + q * TWG;
+        uint64_t d = dl[q], st = 0;
         for (uint32_t spins = 0; (uint32_t)(d >> 32) != a.tag; ++spins) {
             __builtin_amdgcn_s_sleep(8);
-            d = ld_sc1(&a.desc[tid]);
+            d = ld_sc1(&a.desc[i]);
             if (spin_expired(spins, st)) { gave_up = true; break; }  // 200 ms: the count is poisoned below
         }
-        Pl = (uint32_t)d;
+        Pl += (uint32_t)d;
     }
     if (gave_up) g_or(a.fail, FAIL_SPIN_TIMEOUT);
     Pl = wave_sum64(Pl);

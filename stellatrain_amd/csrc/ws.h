@@ -17,7 +17,7 @@ constexpr uint32_t TV_TILE = 8192;           // top-k elements per tile (32 KiB)
 constexpr uint32_t TOPK_SUP_CAP = 1024;      // top-k superset entries kept per tile
 constexpr uint32_t TOPK_LIST_CAP = 4096;     // top-k: keys of T's level-2 bin listed for the final select
 constexpr uint32_t TOPK_LIST_TILES = 8192;   // ... when the bucket has at most this many tiles (64 Mi floats)
-constexpr uint32_t TV_MAXG = 512;            // threshold-v ranges (workgroups) per call
+constexpr uint32_t TV_MAXG = 2048;           // threshold-v ranges (workgroups) per call
 constexpr uint32_t TV_SCAP = 4096;           // threshold-v qualifiers listed per range (32 KiB of LDS)
 constexpr uint32_t TV_MAXNG = 16384;         // threshold-v chunk groups (32 chunks of 32 KiB) per call at most
 
