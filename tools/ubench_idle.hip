@@ -35,6 +35,16 @@ __global__ void __launch_bounds__(512) k_idle(const unsigned *flag, unsigned *ou
     }
 }
 
+struct Big {  // a 1.5 KiB argument block, like the fill launch's
+    const unsigned *flag;
+    unsigned *out;
+    unsigned pad[376];
+};
+__global__ void __launch_bounds__(512) k_idle_big(Big b) {
+    if (__syncthreads_or(b.flag[threadIdx.x & 63] != 1u)) return;
+    b.out[threadIdx.x] = b.pad[threadIdx.x % 376];
+}
+
 int main() {
     const size_t n = 16u << 20, n4 = n / 4;
     const int NB = 16;
@@ -79,6 +89,13 @@ int main() {
     run("stream + idle 512 WG, no scratch", [&](float *b) {
         k_stream<<<G, 256>>>((const float4 *)b, n4, out);
         k_idle<0><<<512, 512>>>(flag, out, 3);
+    });
+    Big big{};
+    big.flag = flag;
+    big.out = out;
+    run("stream + idle 72 WG, 1.5 KiB argument block", [&](float *b) {
+        k_stream<<<G, 256>>>((const float4 *)b, n4, out);
+        k_idle_big<<<72, 512>>>(big);
     });
     return 0;
 }
