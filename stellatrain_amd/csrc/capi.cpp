@@ -822,7 +822,33 @@ int stg_codec_compress_wire_batch_device(stg_codec_t h, const stg_bucket_t *buck
         if (rc) return rc;
         if (flags[i] & ~3) return fail(STG_ERR_INVALID, "unknown wire flag bits");
     }
-    return run_tv16(h, buckets, nbuckets, static_cast<hipStream_t>(stream), nullptr, nullptr, flags);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // One bucket of 16-64 MiB: the one-bucket launch with its in-scan finish
+    // (tv16lf2.h, which has no wire instance) into the workspace's staging,
+    // then the separate packing -- 30.9 against 35.5 us fused for 64 MiB fp16
+    // (profiles/r05_bench_configs_end.jsonl).  STG_WIRE_LONE_FUSED=1: fused.
+    static const bool lone_fused = getenv("STG_WIRE_LONE_FUSED") && atoi(getenv("STG_WIRE_LONE_FUSED")) == 1;
+    if (nbuckets == 1 && flags[0] && !lone_fused && buckets[0].n >= (size_t(1) << 22) &&
+        buckets[0].n <= (size_t(1) << 24)) {
+        const stg_bucket_t &b = buckets[0];
+        HIP_TRY(hipSetDevice(h->device));
+        Workspace *ws = nullptr;
+        int rc = h->workspace(s, &ws);
+        if (rc) return rc;
+        stg_bucket_t t = b;
+        {
+            std::lock_guard<std::mutex> g(ws->mu);
+            if ((rc = ws->ensure(1, 1, std::max<size_t>(b.idx_cap, 1)))) return rc;
+            t.d_idx = ws->d.stage_pos;
+            t.d_val = ws->d.stage_val;
+            t.val_cap = t.idx_cap;
+        }
+        if ((rc = run_tv16(h, &t, 1, s))) return rc;
+        const size_t numel = std::min<size_t>(b.idx_cap, b.n);  // the pairs the fill writes
+        HIP_TRY(stg::launch_wire_encode(t.d_idx, t.d_val, numel, (uint32_t)flags[0], b.d_idx, b.d_val, h->num_cu, s));
+        return STG_OK;
+    }
+    return run_tv16(h, buckets, nbuckets, s, nullptr, nullptr, flags);
 }
 
 int stg_merge_gather_compress_device(stg_codec_t h, const stg_bucket_t *bucket, float *d_residual,
