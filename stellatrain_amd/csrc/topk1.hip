@@ -199,7 +199,10 @@ __device__ __forceinline__ bool pick_exact(const T1Args &A, T1Ldf &L, Pick &P) {
     uint32_t c[PER], s = 0, hi = tid < TK2_HI ? ldw<COH>(&C->hi[tid][0]) : 0u;
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {  // top-down: thread tid holds coarse bins 1023 - (PER tid + j)
-        c[j] = ldw<COH>(&C->coarse[coarse_word(TK2_COARSE - 1u - (PER * tid + j))]);
+        const uint32_t cw = coarse_word(TK2_COARSE - 1u - (PER * tid + j));
+        c[j] = 0;
+#pragma unroll
+        for (uint32_t sh = 0; sh < TK2_CSHARDS; ++sh) c[j] += ldw<COH>(&C->coarse[sh][cw]);
         s += c[j];
     }
     uint32_t th, tband;
@@ -587,7 +590,9 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(7, 
                 } else {
                     const uint32_t f = key - B.F;
                     __hip_atomic_fetch_add(gp(&A.fine[f]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_fetch_add(gp(&C->coarse[coarse_word(f >> TK2_CSH)]), 1u, __ATOMIC_RELAXED,
+                    // (TK2_CSHARDS copies: every tile's band atomics on 64 lines serialised there)
+                    __hip_atomic_fetch_add(gp(&C->coarse[tile % TK2_CSHARDS][coarse_word(f >> TK2_CSH)]), 1u,
+                                           __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
             }

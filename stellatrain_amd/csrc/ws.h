@@ -118,6 +118,10 @@ constexpr uint32_t TK1_LINE = 32;   // words per 128-byte line: every shard coun
 constexpr uint32_t TK2_FINE = 1u << 18;               // band bins: one per ulp
 constexpr uint32_t TK2_CSH = 8;                       // coarse bins: 256 ulps
 constexpr uint32_t TK2_COARSE = TK2_FINE >> TK2_CSH;  // 1024
+#ifndef STG_TK2_CSHARDS
+#define STG_TK2_CSHARDS 1  // 4 and 8 copies measured slower (profiles/r05_topk_finish_ab.jsonl)
+#endif
+constexpr uint32_t TK2_CSHARDS = STG_TK2_CSHARDS;     // copies of the coarse bins (each tile adds into one)
 constexpr uint32_t TK2_HI = 16;                       // shards of the count of keys above the band
 constexpr uint32_t TK2_REG = 32;                      // superset regions (tile mod 32), an offset counter each
 #ifndef STG_TK2_UT
@@ -139,7 +143,7 @@ struct alignas(128) TopkCtl {
     uint32_t utk[TK1_LINE];                    // emission units taken
     uint32_t hi[TK2_HI][TK1_LINE];             // keys >= H, by tile % TK2_HI
     uint32_t shn[TK2_REG][TK1_LINE];           // superset entries placed in region tile % TK2_REG
-    uint32_t coarse[TK2_COARSE];               // band keys per 256 ulps
+    uint32_t coarse[TK2_CSHARDS][TK2_COARSE];  // band keys per 256 ulps, by tile % TK2_CSHARDS
     uint64_t udesc[TK2_UNITS];                 // emission unit u: bit 63 | > T count << 32 | == T count
 };
 
