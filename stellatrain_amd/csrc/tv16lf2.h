@@ -140,6 +140,9 @@ __device__ __forceinline__ float4 ld_sc1_f4(const float4 *base, uint32_t bytes, 
 // it.  Afterwards qp16[c] holds min(qualifying lines before chunk c, 65535):
 // exact wherever it is below lim (lim = dst_len / 16 + 1 < 2^16 on this path,
 // LMAXC chunks of LCHUNK lines, k <= n), which is all the roles use.
+#ifndef STG_LF2_POLL_SLEEP
+#define STG_LF2_POLL_SLEEP 2  // s_sleep between the finishers' descriptor polls (64 cycles a unit)
+#endif
 template <bool WH>
 __device__ __forceinline__ void lf2_decide(Lf2Lds &L, Lf2Dec &D, uint32_t (&h)[4]) {
     const Lf2Args &A = L.a;
@@ -169,7 +172,7 @@ __device__ __forceinline__ void lf2_decide(Lf2Lds &L, Lf2Dec &D, uint32_t (&h)[4
                 D.ok = false;
                 return;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(STG_LF2_POLL_SLEEP);
         }
         if (WH && (h0 + 1) * RH * LF2_WG >= nc) {  // every chunk listed: the window histogram is final
 #pragma unroll
