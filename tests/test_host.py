@@ -197,3 +197,24 @@ def test_no_unmarked_barrier_under_branch_in_ticket_loops():
     assert not bad, bad
     # the checker itself finds the pattern
     assert _barriers_under_branches_in_ticket_loops("for (;;) { if (u == 3) { __syncthreads(); } }")
+
+
+def test_topk_argument_copy_names_every_field():
+    """tk_one copies its argument block into LDS field by field (topk1.hip: a
+    struct copy compiled to a scratch store of the whole block in every
+    thread); a field added to T1Args and missing from the copy would read
+    uninitialised LDS."""
+    import re
+    src = open(os.path.join(ROOT, "stellatrain_amd", "csrc", "topk1.hip")).read()
+    body = src[src.index("struct T1Args {"):]
+    body = body[:body.index("};")]
+    fields = []
+    for line in body.splitlines()[1:]:
+        decl = line.split("//")[0].strip().rstrip(";")
+        if not decl:
+            continue
+        m = re.match(r"^(?:const\s+)?[\w:]+\s*\**\s*(.*)$", decl)
+        fields += [f.strip().lstrip("*").strip() for f in m.group(1).split(",") if f.strip()]
+    assert len(fields) > 20, fields
+    missing = [f for f in fields if f"A.{f} = Ak.{f};" not in src]
+    assert not missing, missing
