@@ -546,7 +546,10 @@ __device__ __forceinline__ void tk2_finish(const T1Args &A, T1Ldf &L, uint32_t u
 // previous hinted call's control block (from its second line on) and of the
 // fine bins that call's band touched (ctl_next keeps the band: [0, H - F)).
 template <bool VEC>
-__global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(7, 8))) tk2_stream(const T1Args A) {
+#ifndef STG_TK2_WPE
+#define STG_TK2_WPE 7  // tk2_stream waves per SIMD (8: 64 VGPRs with spills, measured slower in round 4)
+#endif
+__global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(STG_TK2_WPE, 8))) tk2_stream(const T1Args A) {
     __shared__ T1Ldf L;
     __shared__ uint32_t s_off, s_hi;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, tile = blockIdx.x, nt = A.nt;
