@@ -167,8 +167,16 @@ struct Workspace {
         return STG_OK;
     }
 
-    // one-bucket path lists (tv16lone.hip): per chunk a count pair and the
-    // qualifying / window line lists; written before they are read in every call
+    // one-bucket path lists (tv16lone.hip): per chunk a tagged count pair and
+    // the qualifying / window line lists.  The finish inside the scan launch
+    // (tv16lf2.h) POLLS the count pairs while chunks are still being listed and
+    // takes a pair as this call's once its high word equals the call tag, so
+    // the pairs are zeroed on (re)allocation: recycled device memory (a freed
+    // workspace's pairs, whose tags restart at 1 in every workspace) could
+    // otherwise already hold a live tag with another call's counts.  Tags are
+    // >= 1 and only this workspace writes its pairs afterwards, so no stale
+    // pair ever matches a later call.  The lists themselves are read only
+    // behind a matched pair.
     int ensure_lone(size_t nc) {
         if (nc <= cap_lone) return STG_OK;
         HIP_TRY(hipStreamSynchronize(stream));
@@ -186,6 +194,15 @@ struct Workspace {
         HIP_TRY(hipMalloc(&d.lq, c * stg::LQCAP * sizeof(uint32_t)));
         HIP_TRY(hipMalloc(&d.lw, c * stg::LWCAP * sizeof(uint2)));
         HIP_TRY(hipMalloc(&d.lv, c * stg::LQCAP * 4 * sizeof(float4)));
+        static const bool stale = getenv("STG_DEBUG_LDESC_STALE") && atoi(getenv("STG_DEBUG_LDESC_STALE")) == 1;
+        if (stale) {  // diagnostics: what a recycled block looks like (every pair tagged 1..8, counts 0)
+            std::vector<uint2> p(c);
+            for (size_t i = 0; i < c; ++i) p[i] = make_uint2(0u, 1u + (uint32_t)(i & 7u));
+            HIP_TRY(hipMemcpyAsync(d.ldesc, p.data(), c * sizeof(uint2), hipMemcpyHostToDevice, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+        } else {
+            HIP_TRY(hipMemsetAsync(d.ldesc, 0, c * sizeof(uint2), stream));
+        }
         cap_lone = c;
         return STG_OK;
     }

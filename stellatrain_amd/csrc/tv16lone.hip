@@ -185,7 +185,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
             uint64_t st0 = 0;
             for (uint32_t spins = 0; lds_ld(&L.fin[sl]) < j - 1; ++spins) {
                 __builtin_amdgcn_s_sleep(1);
-                if (spin_expired(spins, st0)) break;  // intra-workgroup: cannot time out while the wave runs
+                // intra-workgroup (the finalizing wave runs): a timeout means a
+                // broken wave, and the slot may still be in use, so the call
+                // is marked failed (poisoned count, failure word) before the
+                // wave goes on and its lists can no longer be trusted
+                if (spin_expired(spins, st0)) {
+                    if (lane == 0) { g_or(A.fail, FAIL_SPIN_TIMEOUT); st_sc1(A.count_out, POISON_COUNT); }
+                    break;
+                }
             }
         }
         const uint32_t L0 = c * LCHUNK;

@@ -21,10 +21,19 @@ def assert_same_pairs(idx_a, val_a, idx_b, val_b, n: int):
     np.testing.assert_array_equal(bits(val_a[:n])[oa], bits(val_b[:n])[ob])
 
 
-def assert_same_stream(idx_a, val_a, idx_b, val_b, n: int):
-    """Bit-exact equality of the first n pairs in order."""
-    np.testing.assert_array_equal(np.asarray(idx_a[:n], np.uint32), np.asarray(idx_b[:n], np.uint32))
-    np.testing.assert_array_equal(bits(val_a[:n]), bits(val_b[:n]))
+def assert_same_stream(idx_a, val_a, idx_b, val_b, n: int, what: str = ""):
+    """Bit-exact equality of the first n pairs in order.  On a mismatch the
+    message names `what` (side, call, regime ...), the first differing
+    position, the number of differing entries and the last indices of both."""
+    ia, ib = np.asarray(idx_a[:n], np.uint32), np.asarray(idx_b[:n], np.uint32)
+    va, vb = bits(val_a[:n]), bits(val_b[:n])
+    bad = np.flatnonzero((ia != ib) | (va != vb)) if ia.size == ib.size else np.arange(n)
+    if bad.size:
+        f = int(bad[0])
+        raise AssertionError(
+            f"{what}: {bad.size} of {n} pairs differ, first at {f} "
+            f"(idx {ia[f:f + 4].tolist()} vs {ib[f:f + 4].tolist()}); "
+            f"stream ends {ia[-3:].tolist()} vs {ib[-3:].tolist()}")
 
 
 def canonical_heap_order(idx, val, head: int, count: int, src: np.ndarray, oracle):

@@ -60,18 +60,21 @@ def test_gather_fused_matches_separate(gpu, oracle, n, N, with_resid):
             else:
                 cnt_s = sep.compress_async("g@w", g_s[0], k, i_s, v_s)
             torch.cuda.synchronize()
-            assert int(cnt_f.item()) == int(cnt_s[0].item()), c
-            np.testing.assert_array_equal(i_f.cpu().numpy(), i_s.cpu().numpy())
-            np.testing.assert_array_equal(v_f.cpu().numpy().view(np.uint32), v_s.cpu().numpy().view(np.uint32))
+            # each side against the oracle on the reference's sum first, so a
+            # failure names the side that is wrong
+            x = _np_gather(srcs, r_np)
+            t_in = oracle.tv16_state(ho, "g@w")[0] if c else None
+            co, io, vo = oracle.tv16_compress(ho, "g@w", x, k)
+            t_out = oracle.tv16_state(ho, "g@w")[0]
+            regime = "first call" if not c else ("B" if t_out < t_in else "A")  # (B decays t by 1 %)
+            what = f"call {c} (n={n}, N={N}, resid={with_resid}, t_in={t_in}, oracle count {co}, regime {regime})"
+            for side, cnt, ii, vv in (("fused", cnt_f, i_f, v_f), ("separate", cnt_s[0], i_s, v_s)):
+                assert int(cnt.item()) == co, f"{side} count {int(cnt.item())} != {co}: {what}"
+                assert_same_stream(ii.cpu().numpy().view(np.uint32), vv.cpu().numpy(), io, vo, co, f"{side} vs oracle, {what}")
             np.testing.assert_array_equal(g_f[0].cpu().numpy().view(np.uint32), g_s[0].cpu().numpy().view(np.uint32))
             if with_resid:
                 np.testing.assert_array_equal(r_f.cpu().numpy().view(np.uint32), r_s.cpu().numpy().view(np.uint32))
-            assert np.float32(fused.state("g@w")[0]) == np.float32(sep.state("g@w")[0])
-            # the oracle on the reference's sum
-            x = _np_gather(srcs, r_np)
-            co, io, vo = oracle.tv16_compress(ho, "g@w", x, k)
-            assert int(cnt_f.item()) == co
-            assert_same_stream(i_f.cpu().numpy().view(np.uint32), v_f.cpu().numpy(), io, vo, co)
+            assert np.float32(fused.state("g@w")[0]) == np.float32(sep.state("g@w")[0]), what
             if with_resid:
                 r_np = r_f.cpu().numpy().copy()
         fused.check_device()

@@ -27,6 +27,8 @@ for s in "$@"; do
         tests) step tests 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
         tests_all) step tests_all 900 python -u -m pytest tests -v -m gpu --timeout 120 --timeout-method thread ;;
         tests_tv16) step tests_tv16 600 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_coresidency.py tests/test_gpu_fill_modes.py -v -m gpu --timeout 120 --timeout-method thread ;;
+        stale_ctl)  # negative control: the one-bucket count pairs pre-tagged as recycled memory would be
+            STG_DEBUG_LDESC_STALE=1 step stale_ctl 300 python -u -m pytest tests/test_gpu_gather_fused.py -v -m gpu --timeout 120 --timeout-method thread ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
         bench) step bench 400 python bench.py ;;
         bench_jitter) step bench_jitter 400 python bench.py --jitter 0.05 --no-cpu-baseline ;;
