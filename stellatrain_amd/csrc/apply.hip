@@ -771,18 +771,12 @@ hipError_t launch_scatter_merge(const uint32_t *idx, const float *val, size_t pe
                                            w1.desc ? w1.ticket : nullptr);
         const uint32_t nt = (uint32_t)((per_rank + MARK_TILE - 1) / MARK_TILE);
         if (w1.desc) {  // count and emit in one launch (tagged tile counts, look-back)
-            static const uint32_t wp = [] {
-                const int x = getenv("STG_MERGE_WP") ? atoi(getenv("STG_MERGE_WP")) : 4;
-                return x == 16 ? 16u : x == 2 ? 2u : x == 1 ? 1u : 4u;
-            }();
+            constexpr uint32_t wp = 4;  // 1,024-pair tiles (2 / 4 / 16 pairs per thread measured no faster)
             const uint32_t nt1 = (uint32_t)((per_rank + wp * STG_WG - 1) / (wp * STG_WG));
             Win1Args a{idx, val, per_rank, n, nt1, win, w1.desc, w1.ticket, 0ull /* win_mark zeroed it */, w1.tag,
                        out_idx, out_val, out_count, w1.fail, w1.dup, w1.sgd != nullptr,
                        w1.sgd ? *w1.sgd : SgdLaunch{}, w1.adam != nullptr, w1.adam ? *w1.adam : AdamLaunch{}};
-            if (wp == 16) win_emit1t<16><<<nt1, STG_WG, 0, s>>>(a);
-            else if (wp == 2) win_emit1t<2><<<nt1, STG_WG, 0, s>>>(a);
-            else if (wp == 1) win_emit1t<1><<<nt1, STG_WG, 0, s>>>(a);
-            else win_emit1t<4><<<nt1, STG_WG, 0, s>>>(a);
+            win_emit1t<wp><<<nt1, STG_WG, 0, s>>>(a);
             if (w1.grid_out) *w1.grid_out = nt1;
             return hipGetLastError();
         }

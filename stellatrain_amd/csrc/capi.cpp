@@ -61,8 +61,6 @@ struct Workspace {
     // threshold-v: the ticket's value at the next call, the last call's
     // range-descriptor tag and the descriptor block last zeroed (tile_cnt, its size)
     uint64_t tv_base = 0;
-    uint32_t tv_ng[2] = {0, 0};  // threshold-v: chunk groups the last call of each parity used
-    uint32_t tv_par = 0;
     uint32_t tv_tag = 0;
     uint32_t *tv_desc = nullptr;
     size_t tv_desc_cap = 0;
@@ -74,6 +72,11 @@ struct Workspace {
     size_t cap_out = 0;
     uint32_t *h_count = nullptr;
     uint32_t *pinned_count = nullptr;
+    // one-bucket wire path staging (stg_codec_compress_wire_batch_device)
+    std::mutex wire_mu;
+    uint32_t *wst_pos = nullptr;
+    float *wst_val = nullptr;
+    size_t cap_wst = 0;
 
     ~Workspace() {
         (void)hipSetDevice(device);
@@ -93,6 +96,8 @@ struct Workspace {
         (void)hipFree(h_idx);
         (void)hipFree(h_val);
         (void)hipFree(h_count);
+        (void)hipFree(wst_pos);
+        (void)hipFree(wst_val);
         if (pinned_count) (void)hipHostFree(pinned_count);
     }
 
@@ -116,9 +121,6 @@ struct Workspace {
         const size_t o_crew = carve(sizeof(stg::CrewCtl) * stg::MAX_BATCH);
         const size_t o_tkc = carve(sizeof(stg::TopkCtl) * 2);
         const size_t o_tkf = carve(sizeof(uint32_t) * 2 * stg::TK2_FINE);
-        const size_t o_tkd = carve(sizeof(uint64_t) * stg::TOPK_LIST_TILES);
-        const size_t o_tku = carve(sizeof(uint32_t) * (2 * stg::TK2_UNITS + 4));
-        const size_t o_tvg = carve(sizeof(uint32_t) * (4 * stg::TV_MAXNG + 1));
         HIP_TRY(hipMalloc(&fixed, off));
         // zeroed on this workspace's stream: the launches that read the
         // control block are ordered after it (a plain hipMemset runs on the
@@ -138,9 +140,6 @@ struct Workspace {
         d.crew = reinterpret_cast<stg::CrewCtl *>(b + o_crew);
         d.tkctl = reinterpret_cast<stg::TopkCtl *>(b + o_tkc);
         d.tkfine = reinterpret_cast<uint32_t *>(b + o_tkf);
-        d.tkdesc = reinterpret_cast<uint64_t *>(b + o_tkd);
-        d.tkdone = reinterpret_cast<uint32_t *>(b + o_tku);
-        d.tvg = reinterpret_cast<uint32_t *>(b + o_tvg);
         return STG_OK;
     }
 
@@ -204,6 +203,16 @@ struct Workspace {
             HIP_TRY(hipMemsetAsync(d.ldesc, 0, c * sizeof(uint2), stream));
         }
         cap_lone = c;
+        return STG_OK;
+    }
+
+    int ensure_wire_stage(size_t n) {  // (caller holds wire_mu)
+        size_t c = cap_wst;
+        int rc;
+        if ((rc = grow(wst_pos, c, n))) return rc;
+        c = cap_wst;
+        if ((rc = grow(wst_val, c, n))) return rc;
+        cap_wst = c;
         return STG_OK;
     }
 
@@ -347,14 +356,9 @@ std::string state_key(Method m, const char *key, const void *src) {
 
 // Device-wide admission of thresholdv16 launches.  No launch waits on a
 // workgroup that is not running (chunks are taken dynamically), so admission
-// is a throughput policy, not a correctness one.
-//  * STG_TV16_SERIAL=1 runs scans one at a time per device: a launch's scan
-//    kernel waits for the previous launch's scan when that was on another
-//    stream, so the previous launch's fill workgroups (which fit beside two
-//    scan workgroups on a CU) run under the next scan.  Off by default: the
-//    event hand-off between streams costs more than it hides, and launches
-//    from three or four streams overlap each other's tails and fills anyway
-//    (profiles/r02_streams.jsonl).
+// is a throughput policy, not a correctness one.  (Scans one at a time per
+// device, each waiting for the previous one's on another stream, measured
+// slower: profiles/r02_streams.jsonl.)
 //  * STG_TV16_INFLIGHT (1-4; default unlimited) launches per device in
 //    flight: a launch on stream s first makes s wait for the oldest in-flight
 //    launch of another stream when the lane is full.  Unlimited (the default)
@@ -365,14 +369,8 @@ struct FusedLane {
     std::mutex mu;
     std::vector<std::pair<hipEvent_t, hipStream_t>> inflight;  // oldest first
     std::vector<hipEvent_t> pool;
-    hipEvent_t scan_ev = nullptr;  // recorded after the last launch's scan
-    hipStream_t scan_stream = nullptr;
 };
 
-bool tv16_serial() {
-    static const bool v = getenv("STG_TV16_SERIAL") && atoi(getenv("STG_TV16_SERIAL")) == 1;
-    return v;
-}
 FusedLane g_lanes[64];
 
 uint32_t fused_inflight() {  // 0: unlimited
@@ -450,34 +448,27 @@ int launch_tv16_group(stg_codec *h, Workspace *ws, std::vector<stg::Tv16Bucket> 
     const uint32_t inflight = fused_inflight();
     constexpr uint32_t XCDS = 8;
     // Every launch may use the whole chip (two scan workgroups per CU): with
-    // dynamic chunk takes, the workgroups of concurrent launches
-    // simply interleave as slots free up (STG_TV16_SHARE=1 splits the slots
-    // evenly between the in-flight launches instead).
-    static const bool share = getenv("STG_TV16_SHARE") && atoi(getenv("STG_TV16_SHARE")) == 1;
-    a.max_wg = share ? std::max<uint32_t>(XCDS, (uint32_t)(2 * h->num_cu) / XCDS / (inflight ? inflight : 4u) * XCDS)
-                     : (uint32_t)(2 * h->num_cu);
+    // dynamic chunk takes, the workgroups of concurrent launches simply
+    // interleave as slots free up (an even split of the slots between the
+    // in-flight launches measured no faster).
+    a.max_wg = (uint32_t)(2 * h->num_cu);
+    (void)XCDS;
     a.desc_cap = (uint32_t)std::min<size_t>(ws->cap_desc, 0xffffffffu);
     a.lone_cap = (uint32_t)ws->cap_lone;
     a.lone_calls = &ws->lone_calls;
-    if (!inflight && !tv16_serial()) {  // no admission: nothing to track
+    if (!inflight) {  // no admission: nothing to track
         HIP_TRY(stg::launch_tv16(a, ws->d, s));
         grp.clear();
         return STG_OK;
     }
     FusedLane &lane = g_lanes[h->device & 63];
     std::lock_guard<std::mutex> lg(lane.mu);
-    const size_t max_inflight = inflight ? inflight : 64;
+    const size_t max_inflight = inflight;
     while (lane.inflight.size() >= max_inflight) {
         auto old = lane.inflight.front();
         lane.inflight.erase(lane.inflight.begin());
         if (old.second != s) HIP_TRY(hipStreamWaitEvent(s, old.first, 0));
         lane.pool.push_back(old.first);
-    }
-    if (tv16_serial()) {
-        if (lane.scan_ev && lane.scan_stream != s) HIP_TRY(hipStreamWaitEvent(s, lane.scan_ev, 0));
-        if (!lane.scan_ev) HIP_TRY(hipEventCreateWithFlags(&lane.scan_ev, hipEventDisableTiming));
-        a.scan_done = lane.scan_ev;  // a wait enqueued above keeps the record it saw
-        lane.scan_stream = s;
     }
     HIP_TRY(stg::launch_tv16(a, ws->d, s));
     hipEvent_t done;
@@ -549,12 +540,6 @@ int ef_after(stg_codec *h, const stg_bucket_t &b, float *resid, bool fused, hipS
     return STG_OK;
 }
 
-// Top-k in one launch steered by the key's last k-th magnitude (topk1.hip);
-// STG_TOPK_ONE=0: the select's launches (topk.hip) every call
-bool topk_one_launch() {
-    static const bool v = !(getenv("STG_TOPK_ONE") && atoi(getenv("STG_TOPK_ONE")) == 0);
-    return v;
-}
 
 int run_device(stg_codec *h, const char *key, const float *d_src, const void *key_ptr, size_t n, uint32_t k,
                uint32_t *d_idx, size_t idx_cap, float *d_val, size_t val_cap, int32_t idx_offset, uint32_t *d_count,
@@ -582,10 +567,8 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         KeyState *st;
         bool fresh;
         if ((rc = h->slot(state_key(h->method, key, key_ptr), &st, &fresh))) return rc;
-        // chunk lists at sums, counts at tile_cnt, maxima at tile_aux (tv.hip);
-        // STG_TV_PASS=1: range descriptors, two words per range
-        if ((rc = ws->ensure(stg::tv_list_words(n), std::max<size_t>(2 * (size_t)stg::TV_MAXG, stg::tv_chunks(n)), 1)))
-            return rc;
+        // range descriptors (tv.hip): counts at tile_cnt, maxima at tile_aux, two words per range
+        if ((rc = ws->ensure(1, 2 * (size_t)stg::TV_MAXG, 1))) return rc;
         if (ws->tv_desc != ws->d.tile_cnt || ws->tv_desc_cap != ws->cap_tiles) {  // fresh memory: no stale tags
             HIP_TRY(hipMemsetAsync(ws->d.tile_cnt, 0, ws->cap_tiles * sizeof(uint32_t), s));
             HIP_TRY(hipMemsetAsync(ws->d.tile_aux, 0, ws->cap_tiles * sizeof(uint32_t), s));
@@ -595,7 +578,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         if (++ws->tv_tag == 0) ws->tv_tag = 1;
         uint32_t grid = 0;
         stg::TvLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, d_count, st, fresh, h->num_cu, ev,
-                        ws->tv_tag, ws->tv_base, &grid, ws->tv_ng, ws->tv_par ^= 1u};
+                        ws->tv_tag, ws->tv_base, &grid};
         HIP_TRY(stg::launch_tv(a, ws->d, s));
         ws->tv_base += grid;
     } else {
@@ -609,7 +592,7 @@ int run_device(stg_codec *h, const char *key, const float *d_src, const void *ke
         stg::TopkLaunch a{d_src, n, k, (uint32_t)idx_cap, d_idx, d_val, idx_offset, h->method == M_TOPK, d_count,
                           h->num_cu, ev};
         const size_t m = h->method == M_TOPK ? (n + 3) / 4 : n;
-        if (topk_one_launch() && (m + stg::TV_TILE - 1) / stg::TV_TILE <= stg::TOPK_LIST_TILES) {
+        if ((m + stg::TV_TILE - 1) / stg::TV_TILE <= stg::TOPK_LIST_TILES) {
             // one launch, steered by the key's last k-th magnitude (its first call: the select inside it)
             KeyState *st;
             bool fresh;
@@ -843,9 +826,8 @@ int stg_codec_compress_wire_batch_device(stg_codec_t h, const stg_bucket_t *buck
     // One bucket of 16-64 MiB: the one-bucket launch with its in-scan finish
     // (tv16lf2.h, which has no wire instance) into the workspace's staging,
     // then the separate packing -- 30.9 against 35.5 us fused for 64 MiB fp16
-    // (profiles/r05_bench_configs_end.jsonl).  STG_WIRE_LONE_FUSED=1: fused.
-    static const bool lone_fused = getenv("STG_WIRE_LONE_FUSED") && atoi(getenv("STG_WIRE_LONE_FUSED")) == 1;
-    if (nbuckets == 1 && flags[0] && !lone_fused && buckets[0].n >= (size_t(1) << 22) &&
+    // (profiles/r05_bench_configs_end.jsonl).
+    if (nbuckets == 1 && flags[0] && buckets[0].n >= (size_t(1) << 22) &&
         buckets[0].n <= (size_t(1) << 24)) {
         const stg_bucket_t &b = buckets[0];
         HIP_TRY(hipSetDevice(h->device));
@@ -853,13 +835,13 @@ int stg_codec_compress_wire_batch_device(stg_codec_t h, const stg_bucket_t *buck
         int rc = h->workspace(s, &ws);
         if (rc) return rc;
         stg_bucket_t t = b;
-        {
-            std::lock_guard<std::mutex> g(ws->mu);
-            if ((rc = ws->ensure(1, 1, std::max<size_t>(b.idx_cap, 1)))) return rc;
-            t.d_idx = ws->d.stage_pos;
-            t.d_val = ws->d.stage_val;
-            t.val_cap = t.idx_cap;
-        }
+        // staging of its own, held for the whole sequence: another thread on
+        // this stream cannot grow (free) it between the compress and the packing
+        std::lock_guard<std::mutex> g(ws->wire_mu);
+        if ((rc = ws->ensure_wire_stage(std::max<size_t>(b.idx_cap, 1)))) return rc;
+        t.d_idx = ws->wst_pos;
+        t.d_val = ws->wst_val;
+        t.val_cap = t.idx_cap;
         if ((rc = run_tv16(h, &t, 1, s))) return rc;
         const size_t numel = std::min<size_t>(b.idx_cap, b.n);  // the pairs the fill writes
         HIP_TRY(stg::launch_wire_encode(t.d_idx, t.d_val, numel, (uint32_t)flags[0], b.d_idx, b.d_val, h->num_cu, s));

@@ -18,13 +18,9 @@ namespace stg {
 
 namespace {
 
-#ifndef STG_RS_GRIDMUL
-#define STG_RS_GRIDMUL 1  // histogram workgroups per CU (fewer global bin atomics; 2: +7 us on top-k)
-#endif
-#ifndef STG_RS_NCOPY
-#define STG_RS_NCOPY 4
-#endif
-constexpr uint32_t NCOPY = STG_RS_NCOPY;
+constexpr uint32_t kRsGridmul = 1;  // histogram workgroups per CU (fewer global bin atomics; 2: +7 us on top-k)
+constexpr uint32_t kRsNcopy = 4;
+constexpr uint32_t NCOPY = kRsNcopy;
 constexpr uint32_t HWG = 1024;  // rs_hist workgroup: one fat workgroup per CU, few global bin atomics
 
 #ifndef STG_RS_STAMPS
@@ -132,7 +128,7 @@ __global__ void __launch_bounds__(HWG) rs_hist(const float *__restrict__ a, size
 hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros, uint32_t rank,
                                const DevWS &ws, int num_cu, hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
-    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
+    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * kRsGridmul));
     rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
     rs_hist<9, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
     rs_hist<0, 9><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
@@ -144,7 +140,7 @@ hipError_t launch_radix_select(const float *a, size_t m, uint32_t last_mask, uin
 hipError_t launch_radix_level1(const float *a, size_t m, uint32_t last_mask, uint64_t extra_zeros, uint32_t rank,
                                const DevWS &ws, int num_cu, hipStream_t s) {
     const size_t work = (m / 4 + HWG - 1) / HWG;
-    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * STG_RS_GRIDMUL));
+    const uint32_t grid = (uint32_t)std::max<size_t>(1, std::min<size_t>(work, (size_t)num_cu * kRsGridmul));
     rs_hist<20, 11><<<grid, HWG, 0, s>>>(a, m, last_mask, ws.rsel, extra_zeros, rank, ws.misc);
     return hipGetLastError();
 }

@@ -15,17 +15,16 @@
 //               {|x| >= F} (in index order) into region tile % 32 at an offset
 //               taken by one atomic; its count of keys >= H; every band key
 //               into the band histogram, one bin per ulp (and a coarse one per
-//               256 ulps).  One read of the bucket.  Its first NU workgroups,
-//               after their own tiles, finish the call (tk2_finish): once
-//               every tile's descriptor carries the call's tag, each finds T
-//               exactly from the histograms (the count above H, the coarse
-//               bins, one coarse bin's 256 ulps: T is a bin), then as one of
-//               the NU emission units (up to 16 tiles) counts its supersets'
-//               (> T, == T) keys, publishes them, sums the earlier units'
-//               (look-back) and writes its winners in order.
-//   tk_one      returns at once when every unit is done; otherwise (a band
-//               that missed, or a finish that could not run) the same pick and
-//               emission by units in ticket order.
+//               256 ulps).  One read of the bucket.
+//   tk_one      every workgroup finds T exactly from the histograms (the
+//               count above H, the coarse bins, one coarse bin's 256 ulps: T
+//               is a bin), then as one of the NU emission units (up to 16
+//               tiles, units in ticket order) counts its supersets' (> T,
+//               == T) keys, publishes them, sums the earlier units' (look-back)
+//               and writes its winners in order.
+// (The same finish inside the stream launch, by its first NU workgroups,
+// measured 26.5 / 37.5 us per shipped / exact C2 call against 24.4 / 35.0 and
+// was removed in round 6.)
 // A band that misses T, or a superset region that overflowed, takes the
 // select's way inside tk_one (three radix levels over the bucket, per-tile
 // counts, emission re-reading the tiles; units by sharded tickets, every
@@ -127,17 +126,9 @@ struct T1Args {
     uint32_t *fine_next;   // the other parity's (the stream launch zeroes what the previous call touched)
     uint32_t *dbg;         // ws.misc: [38] calls resolved in the band, [39] calls that took the select's way
     uint32_t ut;           // tiles per emission unit (<= TK2_UT): about ER STG_WG superset entries
-    bool force_miss;       // tests (STG_TK1_DEBUG=2): the select's way every call
     bool withhold;         // tests (STG_DEBUG_TK_WITHHOLD=1): unit 0 never publishes its counts, so every
                            // later unit's look-back runs out its bound: the failure path end to end
     bool fixed;            // tile t's superset at slot t / TK2_REG of its region (no offset atomic)
-    // the finish inside the stream launch: its first `fin` workgroups are the
-    // emission units (0: tk_one emits); tile t's descriptor tdesc[t] = tag <<
-    // 32 | superset entries; unit u done in the stream launch: done[u] = tag
-    uint32_t fin;
-    uint64_t *tdesc;
-    uint32_t *done;
-    uint64_t *pick;        // [2] the picker's {tag << 32 | hit}, {keys > T << 32 | T}
 };
 
 constexpr uint32_t ER = 8;  // superset entries per thread per emission round
@@ -396,160 +387,12 @@ __device__ __noinline__ bool emit_unit_call(const T1Args &A, T1Ldf &L, uint32_t 
 // the stream launch
 // ---------------------------------------------------------------------------
 
-#ifndef STG_TK2_SUP_PLAIN
-#define STG_TK2_SUP_PLAIN 0  // A/B diagnostics: plain superset stores with the finish in the stream launch too
-#endif
-#ifndef STG_TK1_SKIPALL
-#define STG_TK1_SKIPALL 0  // A/B diagnostics: tk_one returns at once whenever the stream launch finishes
-#endif
-#ifndef STG_TK2_NOFIN
-#define STG_TK2_NOFIN 0  // A/B diagnostics: no finish code in the stream launch (run with STG_TK2_FIN=0)
-#endif
-#ifndef STG_TK2_ZERO_LATE
-#define STG_TK2_ZERO_LATE 0  // A/B diagnostics: the previous call's zeroing after the tile, not before
-#endif
-
-// The finish inside the stream launch, by emission unit u (one of its first
-// A.fin workgroups, each after its own tile): wait for every tile's
-// descriptor, pick T from the histograms, emit the unit (look-back among the
-// finishing workgroups, all resident: the grid's last ones), then done[u].
-// Any wait that gives up, and a band that missed, leaves done[u] unset: tk_one
-// then runs as the finish (the select's way on a miss).
-__device__ __forceinline__ void tk2_finish(const T1Args &A, T1Ldf &L, uint32_t u) {
-    const uint32_t tid = threadIdx.x, nt = A.nt;
-    const uint32_t t0 = u * A.ut, nT = std::min(A.ut, nt - t0);
-    uint64_t st = 0;
-    auto gave_up = [&]() {
-        if (tid == 0) atomicAdd(&A.dbg[59], 1u);
-    };
-    int r;
-    if (u == 0) {
-        // The picker (the first workgroup): every tile's descriptor, rereading
-        // only the ones not yet seen, then T from the histograms, published
-        // as {tag << 32 | hit} after {keys > T << 32 | T}.  The other
-        // finishers poll that one word with one lane: every finisher reading
-        // the histograms itself put ~100 lines x NU coherent loads in the
-        // memory-side queues.
-        constexpr uint32_t PR = 8, PT = TOPK_LIST_TILES / STG_WG;
-        static_assert(PT <= 32, "a seen bit per tile");
-        uint32_t seen = 0;
-        for (uint32_t sp = 0;; ++sp) {
-            uint32_t miss = 0;
-            for (uint32_t g = 0; g < PT && g * STG_WG < nt; g += PR) {  // uniform
-                uint64_t w[PR];
-#pragma unroll
-                for (uint32_t q = 0; q < PR; ++q) {
-                    const uint32_t t = tid + (g + q) * STG_WG;
-                    w[q] = t < nt && !((seen >> (g + q)) & 1u) ? ld_sc1(&A.tdesc[t]) : (uint64_t)A.tag << 32;
-                }
-#pragma unroll
-                for (uint32_t q = 0; q < PR; ++q) {
-                    if ((uint32_t)(w[q] >> 32) == A.tag) seen |= 1u << (g + q);
-                    else miss = 1;
-                }
-            }
-            if (!__syncthreads_or((int)miss)) break;
-            const bool ex = spin_expired(sp, st);
-            if (__syncthreads_or((int)(tid == 0 && ex))) {  // (uniform) tk_one finishes
-                gave_up();
-                return;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        TK1_STAMP(49);  // the picker saw every tile
-        if (tid == 0) L.v[9] = 0;
-        __syncthreads();
-        Pick P;
-        const bool hit = !A.force_miss && pick_exact<true>(A, L, P);
-        if (tid == 0) {
-            if (hit) {  // the next call's hint (tk_one's rule); no finisher reads the state
-                const float Tp = A.state->t, d = A.state->inc, Tf = u2f(P.T);
-                A.state->t = Tf;
-                A.state->inc = fabsf(Tf - Tp) < 0.25f * d * Tp ? fmaxf(0.75f * d, D_MIN) : fminf(d, D_MAX);
-                atomicAdd(&A.dbg[38], 1u);
-                atomicAdd(&A.dbg[49], 1u);  // ... finished inside the stream launch
-                st_sc1(&A.pick[1], (uint64_t)P.gt << 32 | P.T);
-                vm_drain();
-            } else {
-                atomicAdd(&A.dbg[58], 1u);
-            }
-            st_sc1(&A.pick[0], (uint64_t)A.tag << 32 | (hit ? 1u : 0u));
-        }
-        TK1_STAMP(42);  // the pick published
-        if (!hit) return;  // (uniform) tk_one: the select's way
-        auto known = [&](uint32_t &t, uint64_t &ne) -> int {
-            t = P.T;
-            ne = (uint64_t)A.k - P.gt;
-            return 1;
-        };
-        r = emit_unit<true>(A, L, 0, known, true);  // (pick_exact loaded unit 0's tiles)
-    } else {
-        // the unit's own tiles described, then its supersets' first round
-        // loaded while the pick is awaited (emit_unit calls `wait` with them
-        // in flight)
-        for (uint32_t sp = 0;; ++sp) {
-            const bool miss = tid < nT && (uint32_t)(ld_sc1(&A.tdesc[t0 + tid]) >> 32) != A.tag;
-            if (!__syncthreads_or((int)miss)) break;
-            const bool ex = spin_expired(sp, st);
-            if (__syncthreads_or((int)(tid == 0 && ex))) {  // (uniform) tk_one finishes
-                gave_up();
-                return;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        auto wait = [&](uint32_t &t, uint64_t &ne) -> int {
-            if (tid == 0) {
-                uint64_t w = ld_sc1(&A.pick[0]), st2 = 0;
-                uint32_t ok = 1;
-                for (uint32_t sp = 0; (uint32_t)(w >> 32) != A.tag; ++sp) {
-                    __builtin_amdgcn_s_sleep(4);
-                    w = ld_sc1(&A.pick[0]);
-                    if (spin_expired(sp, st2)) { ok = 2; break; }
-                }
-                if (ok == 1 && !(w & 1u)) ok = 0;
-                if (ok == 1) {
-                    const uint64_t x = ld_sc1(&A.pick[1]);
-                    L.v[5] = (uint32_t)x;
-                    L.v[6] = (uint32_t)(x >> 32);
-                }
-                L.v[8] = ok;
-            }
-            __syncthreads();
-            const uint32_t ok = L.v[8];
-            t = L.v[5];
-            ne = (uint64_t)A.k - L.v[6];
-            __syncthreads();
-            TK1_STAMP_MAX(43);  // the last finisher has the pick
-            if (ok == 2) gave_up();
-            return ok == 1 ? 1 : 0;  // a miss or a wait that gave up: tk_one finishes
-        };
-        r = emit_unit<true>(A, L, u, wait, false);
-    }
-    if (r < 0) {
-        if (tid == 0) {
-            g_or(A.fail, FAIL_SPIN_TIMEOUT);
-            __hip_atomic_fetch_max(gp(A.count_out), POISON_COUNT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    if (r == 0) return;
-    TK1_STAMP_MAX(50);  // the last unit emitted
-    vm_drain();
-    __syncthreads();
-    if (tid == 0) {
-        st_sc1(&A.done[u], A.tag);
-        atomicAdd(&A.dbg[56], 1u);  // units finished inside the stream launch
-    }
-}
-
 // One workgroup per tile.  Before its tile, each zeroes its share of the
 // previous hinted call's control block (from its second line on) and of the
 // fine bins that call's band touched (ctl_next keeps the band: [0, H - F)).
+// Seven waves per SIMD (eight: 64 VGPRs with spills, measured slower in round 4).
 template <bool VEC>
-#ifndef STG_TK2_WPE
-#define STG_TK2_WPE 7  // tk2_stream waves per SIMD (8: 64 VGPRs with spills, measured slower in round 4)
-#endif
-__global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(STG_TK2_WPE, 8))) tk2_stream(const T1Args A) {
+__global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(7, 8))) tk2_stream(const T1Args A) {
     __shared__ T1Ldf L;
     __shared__ uint32_t s_off, s_hi;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6, tile = blockIdx.x, nt = A.nt;
@@ -568,8 +411,13 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(STG
             else f4[i - CW] = make_uint4(0u, 0u, 0u, 0u);
         }
     };
-    if (!STG_TK2_ZERO_LATE || !B.ok) zero_prev();
-    if (!B.ok) return;  // tk_one takes the select's way (band_ok stays 0)
+    zero_prev();
+    if (!B.ok) {  // tk_one takes the select's way: this call's block says so
+        // (its first line is never zeroed, so it would still hold the band of
+        // the hinted call two calls back)
+        if (tile == 0 && tid == 0) st_sc1(&A.ctl->band_ok, 0u);
+        return;
+    }
     if (tile == 0) TK1_STAMP(40);  // the stream launch's first workgroup starts
     TopkCtl *const C = A.ctl;
     if (tile == 0 && tid == 0) {
@@ -649,26 +497,10 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(STG
                     // launch: plain ones measured 29.5 / 49.7 us per shipped / exact
                     // call and 15 / 55 MB written per call, against 24.5 / 35.3 us and
                     // 7.1 / 8.1 MB (profiles/r05_pmc_topk*_hinted.json)
-                    if (STG_TK2_SUP_PLAIN) dst[slot++] = w;
-                    else st_sc1(&dst[slot++], w);
+                    st_sc1(&dst[slot++], w);
                 }
         }
     }
-    if (STG_TK2_ZERO_LATE) zero_prev();
-    if (!A.fin) return;
-    // the tile's descriptor once its stores and atomics are complete
-    vm_drain();
-    __syncthreads();
-    if (tid == 0) st_sc1(&A.tdesc[tile], (uint64_t)A.tag << 32 | nsup);
-    TK1_STAMP_MAX(41);  // the last tile described
-    if (STG_TK2_NOFIN || tile >= A.fin) return;
-    // The finishers are the grid's FIRST NU workgroups: resident from the
-    // start, they wait (polling lightly) while the other tiles stream, and the
-    // chain starts the moment the last tile lands.  (The last NU, dispatched
-    // last, started it a tile's lifetime late.)  Inlined with everything it
-    // calls: the argument block's fields stay scalar loads; a copy of the
-    // block, or a call taking it, puts it in memory.
-    tk2_finish(A, L, tile);
 }
 
 // A key's first call ran topk.hip's launches: T (rs->prefix) seeds the hint.
@@ -837,15 +669,6 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     // reference to the kernel's argument block would be copied to scratch)
     __shared__ T1Args A;
     const uint32_t tid = threadIdx.x;
-    if (Ak.fin) {  // the stream launch finished every emission unit (read before the argument copy)
-        uint32_t miss = 0;
-        // (plain loads: written by the stream launch, a kernel boundary; sc1
-        // loads of the same few lines by every workgroup queue at the memory side)
-        if (STG_TK1_SKIPALL) return;
-        for (uint32_t i = tid; i < Ak.fin; i += STG_WG) miss |= Ak.done[i] != Ak.tag ? 1u : 0u;
-        if (!__syncthreads_or((int)miss)) return;
-        if (tid == 0) atomicAdd(&Ak.dbg[57], 1u);  // workgroups of tk_one that run after all
-    }
     // the argument block into LDS field by field: `A = Ak` compiled to a private
     // copy of the whole block, stored to scratch by every thread of every
     // workgroup before anything else (~10 MB a launch, ~15 us)
@@ -855,9 +678,8 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
         A.count_out = Ak.count_out; A.fail = Ak.fail; A.state = Ak.state; A.ctl = Ak.ctl; A.ctl_next = Ak.ctl_next;
         A.tag = Ak.tag; A.rs = Ak.rs; A.sup = Ak.sup; A.shard_cap = Ak.shard_cap; A.sup_n = Ak.sup_n;
         A.sup_off = Ak.sup_off; A.tile_gt = Ak.tile_gt; A.tile_eq = Ak.tile_eq; A.fine = Ak.fine;
-        A.fine_next = Ak.fine_next; A.dbg = Ak.dbg; A.ut = Ak.ut; A.force_miss = Ak.force_miss;
-        A.withhold = Ak.withhold; A.fixed = Ak.fixed; A.fin = Ak.fin; A.tdesc = Ak.tdesc; A.done = Ak.done;
-        A.pick = Ak.pick;
+        A.fine_next = Ak.fine_next; A.dbg = Ak.dbg; A.ut = Ak.ut;
+        A.withhold = Ak.withhold; A.fixed = Ak.fixed;
     }
     __syncthreads();
     TopkCtl *const C = A.ctl;
@@ -876,7 +698,7 @@ __global__ void __launch_bounds__(STG_WG) __attribute__((amdgpu_waves_per_eu(4, 
     // round trip overlaps the pick's loads
     const uint32_t NU = (A.nt + A.ut - 1u) / A.ut;
     if (tid == 0) L.v[9] = blockIdx.x < NU ? g_add(&C->utk[0], 1u) : NU;
-    const bool hit = !A.force_miss && pick_exact_call(A, L, P);
+    const bool hit = pick_exact_call(A, L, P);
     if (blockIdx.x == 0) TK1_STAMP(42);  // workgroup 0: pick done
     TK1_STAMP_MAX(43);                   // every workgroup's pick done
     if (hit) {
@@ -1040,10 +862,9 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     // superset regions: the bucket's share of TOPK_SUP_CAP entries per tile, in TK2_REG regions
     // Fixed slots when k is at most 1/16 of the keys (a tile's superset, ~k / nt
     // entries plus the band, stays well under TOPK_SUP_CAP = TV_TILE / 8);
-    // denser calls (and STG_TK2_FIXED=0) take region offsets by atomics, so
-    // that a region's 32 tiles share its space.  Fixed: C2 33.6 -> 33.1 us.
-    static const bool fixed_ok = !(getenv("STG_TK2_FIXED") && atoi(getenv("STG_TK2_FIXED")) == 0);
-    const bool fixed = fixed_ok && (uint64_t)std::min<uint64_t>(a.k, m) * 16u <= m;
+    // denser calls take region offsets by atomics, so that a region's 32
+    // tiles share its space.  Fixed: C2 33.6 -> 33.1 us.
+    const bool fixed = (uint64_t)std::min<uint64_t>(a.k, m) * 16u <= m;
     const uint32_t shard_cap = fixed ? (nt + TK2_REG - 1) / TK2_REG * TOPK_SUP_CAP
                                      : (uint32_t)((size_t)nt * TOPK_SUP_CAP / TK2_REG);
     uint32_t *const sup_n = ws.tile_cnt + 2 * (size_t)nt + 1, *const sup_off = ws.tile_aux + 2 * (size_t)nt + 1;
@@ -1076,37 +897,22 @@ hipError_t launch_topk1(const TopkLaunch &a, const DevWS &ws, KeyState *state, b
     A.tile_eq = ws.tile_aux;
     A.fine = fine;
     // a unit's superset (~ k / nt entries per tile): about `per_unit` entries,
-    // so that the units spread over the CUs (STG_TK1_UNIT: entries per unit)
-    static const uint64_t per_unit =
-        getenv("STG_TK1_UNIT") ? (uint64_t)std::max(64, atoi(getenv("STG_TK1_UNIT"))) : (uint64_t)ER * STG_WG * 3 / 4;
+    // so that the units spread over the CUs
+    constexpr uint64_t per_unit = (uint64_t)ER * STG_WG * 3 / 4;
     A.ut = (uint32_t)std::max<uint64_t>((nt + TK2_UNITS - 1) / TK2_UNITS,
                                         std::min<uint64_t>(TK2_UT, per_unit * nt / std::max<uint64_t>(A.k, 1)));
     A.ut = std::max(1u, std::min(A.ut, TK2_UT));
     A.fine_next = ws.tkfine + (size_t)((tag + 1u) & 1u) * TK2_FINE;
     A.dbg = ws.misc;
     A.fixed = fixed;
-    // the finish inside the stream launch: its first NU workgroups, one per
-    // emission unit, when that leaves most of the grid to the tiles
-    // (off by default: measured 26.5 / 37.5 us per shipped / exact C2 call
-    // against 24.4 / 35.0 with tk_one finishing; STG_TK2_FIN=1 turns it on)
-    static const bool fin_ok = getenv("STG_TK2_FIN") && atoi(getenv("STG_TK2_FIN")) == 1;
     const uint32_t NU = (nt + A.ut - 1u) / A.ut;
-    A.fin = fin_ok && nt >= 2u * NU ? NU : 0u;
-    A.tdesc = ws.tkdesc;
-    A.done = ws.tkdone;
-    A.pick = reinterpret_cast<uint64_t *>(ws.tkdone + 2 * TK2_UNITS);
-    static const int dbg_mode = getenv("STG_TK1_DEBUG") ? atoi(getenv("STG_TK1_DEBUG")) : 0;
-    A.force_miss = dbg_mode == 2;
     static const bool withhold = getenv("STG_DEBUG_TK_WITHHOLD") && atoi(getenv("STG_DEBUG_TK_WITHHOLD")) == 1;
     A.withhold = withhold;
     if (a.ev) (void)hipEventRecord(a.ev[0], s);
     if (vec) tk2_stream<true><<<nt, STG_WG, 0, s>>>(A);
     else tk2_stream<false><<<nt, STG_WG, 0, s>>>(A);
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    // every emission unit has a workgroup of its own (NU <= TK2_UNITS).  (A
-    // grid of just the NU units, for a cheaper idle launch behind the stream
-    // launch's finish, broke the select's way on a miss: FAIL_SELECT at 17
-    // workgroups, tests/test_gpu_alt_paths.py)
+    // every emission unit has a workgroup of its own (NU <= TK2_UNITS)
     const uint32_t G = std::max<uint32_t>(std::min<uint32_t>(nt, (uint32_t)a.num_cu * 2u), NU);
     if (vec) tk_one<true><<<G, STG_WG, 0, s>>>(A);
     else tk_one<false><<<G, STG_WG, 0, s>>>(A);

@@ -49,66 +49,34 @@ namespace stg {
 namespace {
 
 using namespace tv16;
-#ifndef STG_EF_AUX
-#define STG_EF_AUX 2  // cache policy of the fused residual stores (2: nontemporal)
-#endif
+constexpr uint32_t kEfAux = 2;  // cache policy of the fused residual stores (2: nontemporal)
 
-#ifndef STG_TV16_NS
-#define STG_TV16_NS 11
-#endif
-constexpr uint32_t FWG = (STG_TV16_NS + 1) * 64;  // workgroup: the streaming waves + the finisher
+constexpr uint32_t kTv16Ns = 11;
+constexpr uint32_t FWG = (kTv16Ns + 1) * 64;  // workgroup: the streaming waves + the finisher
 constexpr uint32_t FNW = FWG / 64;
-constexpr uint32_t NS = STG_TV16_NS;  // streaming waves 0..NS-1
+constexpr uint32_t NS = kTv16Ns;  // streaming waves 0..NS-1
 constexpr uint32_t FIN = NS;          // the finisher; waves past it (if any) idle
 static_assert(NS + 1 <= FNW && FWG <= 1024, "streaming group + finisher fit the workgroup");
-#ifndef STG_TV16_NBUF
-#define STG_TV16_NBUF 5
-#endif
-#ifndef STG_TV16_SCAN_D
-#define STG_TV16_SCAN_D 3
-#endif
-constexpr uint32_t NBUF = STG_TV16_NBUF;  // LDS buffer sets (slots) in flight per workgroup
+constexpr uint32_t kTv16Nbuf = 5;
+constexpr uint32_t kTv16ScanD = 3;
+constexpr uint32_t NBUF = kTv16Nbuf;  // LDS buffer sets (slots) in flight per workgroup
 constexpr uint32_t CIDR = 2 * NBUF;       // chunk-id ring
-#ifndef STG_TV16_STAGE_B
-#define STG_TV16_STAGE_B 72
-#endif
-#ifndef STG_TV16_WL_B
-#define STG_TV16_WL_B 64
-#endif
-constexpr uint32_t STAGE_B = STG_TV16_STAGE_B;  // qualifying lines staged in LDS per slot (~20 expected at 1%)
-constexpr uint32_t WL_B = STG_TV16_WL_B;  // window candidates listed in LDS per slot
-#ifndef STG_TV16_POLL_SLEEP
-#define STG_TV16_POLL_SLEEP 8  // s_sleep units (64 clocks) between prefix polls
-#endif
-// diagnostics only (timing attribution; wrong results): skip the prefix waits
-// or the ordered emission
-#ifndef STG_TV16_DIAG_NOWAIT
-#define STG_TV16_DIAG_NOWAIT 0
-#endif
-#ifndef STG_TV16_DIAG_NOEMIT
-#define STG_TV16_DIAG_NOEMIT 0
-#endif
-#ifndef STG_TV16_DIAG_STATIC0
-#define STG_TV16_DIAG_STATIC0 0
-#endif
-#ifndef STG_TV16_DIAG_STORES
-#define STG_TV16_DIAG_STORES 0
-#endif
-#ifndef STG_TV16_PRIO
-#define STG_TV16_PRIO 1
-#endif
+constexpr uint32_t kTv16StageB = 72;
+constexpr uint32_t kTv16WlB = 64;
+constexpr uint32_t STAGE_B = kTv16StageB;  // qualifying lines staged in LDS per slot (~20 expected at 1%)
+constexpr uint32_t WL_B = kTv16WlB;  // window candidates listed in LDS per slot
+constexpr uint32_t kTv16PollSleep = 8;  // s_sleep units (64 clocks) between prefix polls
+constexpr uint32_t kTv16Prio = 1;
 constexpr uint32_t GB = 512;        // chunk descriptors gathered per round trip (a 64 MiB bucket has 512)
 // float4 loads in flight per streaming wave: 2 x 14 x 64 x 16 B x SCAN_D per CU
 // (SCAN_D = 3: 84 KiB per CU, just over the ~72 KiB that hides an HBM miss;
 // deeper queues add latency to every exchange round trip -- Little's law)
-constexpr uint32_t SCAN_D_BATCH = STG_TV16_SCAN_D;
+constexpr uint32_t SCAN_D_BATCH = kTv16ScanD;
 // A one-bucket launch (its fill runs after it, nothing else of the codec
 // beside it): each workgroup streams one chunk, so twice the loads in flight
 // halve its round trips; 6 waves per SIMD leave it ~80 VGPRs.
-#ifndef STG_TV16_SCAN_D_LONE
-#define STG_TV16_SCAN_D_LONE 6
-#endif
-constexpr uint32_t SCAN_D_LONE = STG_TV16_SCAN_D_LONE;
+constexpr uint32_t kTv16ScanDLone = 6;
+constexpr uint32_t SCAN_D_LONE = kTv16ScanDLone;
 constexpr uint32_t MAXG = 512;      // workgroups per launch (2 per CU)
 // ---------------------------------------------------------------------------
 // first call: sequential |x| sums per line, last partial line scaled by
@@ -291,7 +259,7 @@ __device__ __forceinline__ void scan_chunk(Ctx &C, uint32_t j, uint32_t k, uint3
         asm volatile("" : "+v"(voff));
         u4v t4;
         t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
-        __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NS * 1024u), 0, STG_EF_AUX /* 2 = nt */);
+        __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NS * 1024u), 0, kEfAux /* 2 = nt */);
     };
     auto load = [&](uint32_t m) -> float4 {
         uint32_t voff = lane_line * 64u + q * 16u;
@@ -448,9 +416,9 @@ __device__ __forceinline__ void prefix_counts(Ctx &C, uint32_t b, uint32_t c, ui
             uint64_t st4 = 0;
             for (uint32_t spins = 0;; ++spins) {
                 const uint64_t pm = __ballot(pend);
-                if (!pm || STG_TV16_DIAG_NOWAIT) break;
+                if (!pm) break;
                 const uint32_t hl = 63u - (uint32_t)__clzll((long long)pm);
-                __builtin_amdgcn_s_sleep(STG_TV16_POLL_SLEEP);
+                __builtin_amdgcn_s_sleep(kTv16PollSleep);
                 if (lane == hl) {
                     a = ld_sc1(&C.A.desc[d.cs + p0 + i].agg);
                     pend = (uint32_t)(a >> 32) != tA;
@@ -507,7 +475,7 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k) {
     const uint32_t kb = d.dst_len / 16, r = d.dst_len % 16;
     const uint32_t lim = kb + (r ? 1u : 0u);
     const bool vec = aligned16(d);
-    if (P < lim && qw && !STG_TV16_DIAG_NOEMIT) {
+    if (P < lim && qw) {
         if (qw <= STAGE_B) {
             // every qualifying line is staged in LDS with its line index: its
             // in-chunk rank is the number of staged lines before it; a quad
@@ -601,8 +569,6 @@ __device__ __forceinline__ void finish_chunk(Ctx &C, uint32_t j, uint32_t k) {
             }
         }
     }
-#pragma unroll
-    for (uint32_t x = 0; x < STG_TV16_DIAG_STORES; ++x) st_sc1(C.failp + 60 + (x & 3), 0u);  // diagnostics: extra stores
     release(C, par, j);
 
     // ---- the bucket's last chunk: regime, tail, AIMD, count, decision ----
@@ -686,11 +652,7 @@ tv16_batch(BatchArgs A) {
         // workgroup's slots therefore hold increasing chunks, chunks are taken
         // in order, and a chunk is only ever taken by a running workgroup: no
         // wait in this launch points at a workgroup that is not resident.
-#if STG_TV16_DIAG_STATIC0  // diagnostics only (co-residency dependent): slot 0 = workgroup id when K <= G
-        L.cid[0] = A.K <= C.G ? C.w : g_add(&C.cc()->next, 1u);
-#else
         L.cid[0] = g_add(&C.cc()->next, 1u);
-#endif
         for (uint32_t i = 0; i < CIDR; ++i) { L.cok[i] = 0; L.mid[i] = 0; }
         L.cok[0] = 1;
     }
@@ -709,7 +671,7 @@ tv16_batch(BatchArgs A) {
             scan_chunk<STAGE, EF, LONE ? SCAN_D_LONE : SCAN_D_BATCH>(C, j, k, wave);
         }
     } else if (wave == FIN) {
-        if (STG_TV16_PRIO) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
+        if (kTv16Prio) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
         for (uint32_t j = 0;; ++j) {
             uint64_t st9 = 0;
             for (uint32_t spins = 0; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {
@@ -727,16 +689,14 @@ tv16_batch(BatchArgs A) {
 // Workgroups of a fill launch that order window-miss buckets (tv16wide.h): they
 // exit at once when no bucket of the launch needs them.
 uint32_t crew_batch() {
-    static const uint32_t v = getenv("STG_TV16_CREW") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW"))) : 64u;
-    return v ? std::min(std::max(v, MAX_BATCH + 1u), 1024u) : 0u;  // > MAX_BATCH: see tv16wide.h crew_loop
+    constexpr uint32_t v = 64u;  // > MAX_BATCH: see tv16wide.h crew_loop
+    return v;
 }
 // One-bucket launches: every CU the launch's other workgroups leave (a fill
 // workgroup takes a whole CU's LDS), so that phase A streams at full width.
 uint32_t crew_lone(uint32_t num_cu, uint32_t others) {
-    static const uint32_t v =
-        getenv("STG_TV16_CREW_LONE") ? (uint32_t)std::max(0, atoi(getenv("STG_TV16_CREW_LONE"))) : 1024u;
     const uint32_t room = num_cu > others ? num_cu - others : 0u;
-    return v ? std::min(std::max(std::min(v, room), MAX_BATCH + 1u), 1024u) : 0u;
+    return std::min(std::max(room, MAX_BATCH + 1u), 1024u);
 }
 
 }  // namespace
@@ -748,7 +708,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
     Tv16FillArgs F{};
     uint32_t K = 0;
     static const int dbg_stage = getenv("STG_DEBUG_TV16_STAGE") ? atoi(getenv("STG_DEBUG_TV16_STAGE")) : 0;
-    static const bool lone_ok = !(getenv("STG_TV16_LONE") && atoi(getenv("STG_TV16_LONE")) == 0);
+    constexpr bool lone_ok = true;
     // the one-bucket path: a scan with no waits between workgroups, finished
     // by the fill launch (tv16lone.hip; STG_TV16_LFIN=0: the batched scan)
     static const bool lfin_ok = !(getenv("STG_TV16_LFIN") && atoi(getenv("STG_TV16_LFIN")) == 0);
@@ -862,10 +822,9 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         // the finish inside the scan launch (tv16lf2.h): not under the fused
         // gather (the scan rewrites the bucket) or the wire form
         static const int lf2_env = getenv("STG_TV16_LF2") ? atoi(getenv("STG_TV16_LF2")) : 1;
-        static const uint32_t lf2_fin = (uint32_t)std::max(0, std::min(
-            getenv("STG_TV16_LF2_FIN") ? atoi(getenv("STG_TV16_LF2_FIN")) : 64, (int)LF2_MAXF));
-        static const uint32_t lf2_wk = (uint32_t)std::max(8, std::min(
-            getenv("STG_TV16_LF2_WORKERS") ? atoi(getenv("STG_TV16_LF2_WORKERS")) : 48, (int)LF2_MAXF));
+        // 48 workers + 16 rankers (profiles/r05_lf2_roles_sweep.txt)
+        constexpr uint32_t lf2_fin = 64, lf2_wk = 48;
+        static_assert(lf2_fin <= LF2_MAXF, "roles");
         {
             static const uint32_t fill_mode0 =
                 getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
@@ -893,7 +852,6 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         hipError_t e = launch_tv16_lscan(L, a.num_cu, s);  // (clamps L.fin to what the grid allows)
         if (e != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[1], s);
-        if (a.scan_done && (e = hipEventRecord(a.scan_done, s)) != hipSuccess) return e;
         F.nbk = 1;
         F.epoch = a.epoch;
         F.dec = ws.ctl->dec;
@@ -903,11 +861,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
         F.mode = fill_mode;
         F.lone = true;
-        static const uint32_t helpers =
-            getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
-        static const uint32_t workers = std::max(1, std::min(
-            getenv("STG_TV16_LFIN_WORKERS") ? atoi(getenv("STG_TV16_LFIN_WORKERS")) : 64, 192));
-        (void)helpers;
+        constexpr uint32_t workers = 64;
         static const uint32_t rankers = std::max(0, std::min(
             getenv("STG_TV16_LFIN_RANKERS") ? atoi(getenv("STG_TV16_LFIN_RANKERS")) : 8, 128));
         F.helpers = 0;
@@ -931,9 +885,6 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         F.crew = crew_lone(a.num_cu, workers + rankers);
         F.crew_ctl = ws.crew;
         if ((e = launch_tv16_fill_any(F, s)) != hipSuccess) return e;
-        static const uint32_t noop_g = getenv("STG_DEBUG_NOOP") ? (uint32_t)atoi(getenv("STG_DEBUG_NOOP")) : 0u;
-        static const uint32_t noop_lds = getenv("STG_DEBUG_NOOP_LDS") ? (uint32_t)atoi(getenv("STG_DEBUG_NOOP_LDS")) : 0u;
-        if (noop_g && (e = launch_lone_noop(noop_g, noop_lds, ws.fail, ws.misc + 63, s)) != hipSuccess) return e;
         if (a.ev) (void)hipEventRecord(a.ev[2], s);
         return hipGetLastError();
     }
@@ -948,10 +899,6 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             break;
     }
     if (a.ev) (void)hipEventRecord(a.ev[1], s);
-    if (a.scan_done) {
-        const hipError_t e = hipEventRecord(a.scan_done, s);
-        if (e != hipSuccess) return e;
-    }
     if (dbg_stage != 1 && dbg_stage != 3) {
         // regime-B heap fill: one workgroup per bucket, stream-ordered after the scan
         F.nbk = a.nb;
@@ -963,9 +910,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
             getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
         F.mode = fill_mode;
         F.lone = lone_scan;
-        static const uint32_t helpers =
-            getenv("STG_TV16_FILL_HELPERS") ? (uint32_t)atoi(getenv("STG_TV16_FILL_HELPERS")) : 15u;
-        F.helpers = F.lone ? std::min(helpers, 63u) : 0u;
+        F.helpers = F.lone ? 15u : 0u;
         F.cc = &ws.ctl->cc[a.epoch & 1u];
         F.crew = F.lone ? crew_lone(a.num_cu, F.nbk + F.helpers) : crew_batch();
         F.crew_ctl = ws.crew;

@@ -40,26 +40,13 @@ namespace {
 
 using namespace tv16;
 
-#ifndef STG_EF_AUX
-#define STG_EF_AUX 2  // cache policy of the fused residual stores (2: nontemporal)
-#endif
+constexpr uint32_t kEfAux = 2;  // cache policy of the fused residual stores (2: nontemporal)
 
-// diagnostics only (timing attribution; wrong results): 1 = no per-chunk
-// lists written, 2 = the plain stream (no line sums, no lists)
-#ifndef STG_LSCAN_DIAG
-#define STG_LSCAN_DIAG 0
-#endif
 
 static_assert(LCHUNK <= 512 && LMAXC <= 4096 && LQCAP < 1024, "binned entry packing: chunk:12 | line:9 | qb:10");
 static_assert(LNBIN << 8 == TV16_WIN, "bins of 256 ulps cover the window");
 
-#ifndef STG_LSCAN_PAD
-#define STG_LSCAN_PAD 0  // diagnostics: extra LDS bytes per workgroup (occupancy A/B)
-#endif
 struct LLds {
-#if STG_LSCAN_PAD
-    uint32_t pad_[STG_LSCAN_PAD / 4];
-#endif
     float4 qv[2][LQCAP][4];  // their data (a float4 per lane of the line's quad)
     uint32_t ql[2][LQCAP];  // qualifying lines of the chunk in the slot (unordered)
     uint64_t wl[2][LWCAP];  // window lines: sum bits << 32 | line
@@ -234,7 +221,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
             asm volatile("" : "+v"(voff));
             u4v t4;
             t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
-            __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NW * 1024u), 0, STG_EF_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc_r, voff + m * (NW * 1024u), 0, kEfAux);
         };
         float4 v[D], w[GS ? GS : 1][D];
 #pragma unroll
@@ -271,11 +258,6 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
                         w[e][u] = load_x(e, m0 + u + D);
                     }
                     store_s(m0 + u, x);
-                }
-                if (STG_LSCAN_DIAG == 2) {
-                    v[u] = load(m0 + u + D);
-                    if (__float_as_uint(x.x + x.y + x.z + x.w) == 0x7f800001u) L.qn[sl] = 1;
-                    continue;
                 }
                 uint32_t ll = lane_line;
                 asm volatile("" : "+v"(ll));
@@ -324,45 +306,22 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
         uint32_t old = 0;
         if (lane == 0) old = atomicAdd(&L.done[sl], 1u);
         if (uni(old) == NW - 1) {  // every other wave's list adds were drained first
-            if (STG_LSCAN_DIAG) {
-                if (lane == 0) { L.qn[sl] = 0; L.wn[sl] = 0; L.done[sl] = 0; }
-                lds_drain();
-                if (lane == 0) lds_st(&L.fin[sl], j + 1);
-            } else {
-                finalize(L, A, sl, c, j, tb);
-            }
+            finalize(L, A, sl, c, j, tb);
         }
     }
-    if (!STG_LSCAN_DIAG && !GS && A.fin && blockIdx.x + A.fin >= gridDim.x)
+    if (!GS && A.fin && blockIdx.x + A.fin >= gridDim.x)
         lf2_finish(U.f, A, blockIdx.x + A.fin - gridDim.x, t, inc0);
-}
-
-// diagnostics (STG_DEBUG_NOOP): a launch whose workgroups read one word and
-// exit, to price a follow-on launch that has nothing to do
-__global__ void lone_noop(const uint32_t *w, uint32_t *out) {
-    extern __shared__ uint32_t noop_lds[];
-    if (threadIdx.x == 0 && ld_sc1(w) == 0x12345678u) { noop_lds[0] = 1; out[0] = noop_lds[0]; }
 }
 
 }  // namespace
 
-hipError_t launch_lone_noop(uint32_t grid, uint32_t lds, const uint32_t *w, uint32_t *out, hipStream_t s) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void *>(&lone_noop),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr != hipSuccess) return attr;
-    lone_noop<<<grid, 512, lds, s>>>(w, out);
-    return hipGetLastError();
-}
-
 hipError_t launch_tv16_lscan(LScanArgs &a, int num_cu, hipStream_t s) {
     if (!a.nc) { a.fin = 0; return hipSuccess; }
-    // shape (diagnostics: STG_TV16_LSHAPE): 0 = 4 waves, 8 float4 loads in
-    // flight per lane (the whole 32 KiB chunk), eight workgroups per CU (the
-    // fastest single-launch 64 MiB read measured, tools/ubench_stream.hip);
-    // 1 = 8 waves, 4 loads, four per CU
-    static const int shape = getenv("STG_TV16_LSHAPE") ? atoi(getenv("STG_TV16_LSHAPE")) : 0;
+    // 4 waves, 8 float4 loads in flight per lane (the whole 32 KiB chunk),
+    // eight workgroups per CU: the fastest single-launch 64 MiB read measured
+    // (tools/ubench_stream.hip; 8 waves with 4 loads, four per CU: no faster)
     const bool ef = a.resid != nullptr;
-    const uint32_t per_cu = shape == 1 ? 4u : 8u;
+    constexpr uint32_t per_cu = 8u;
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(a.nc, per_cu * (uint32_t)num_cu));
     // the finish's roles: the last `fin` workgroups of the grid, at least
     // nwk + 1 of them (a ranker); else the fill launch finishes the call
@@ -380,9 +339,6 @@ hipError_t launch_tv16_lscan(LScanArgs &a, int num_cu, hipStream_t s) {
             if (ef) tv16_lscan<true, 4, 1, GATHER_MAX><<<G, 256, 0, s>>>(a);
             else tv16_lscan<false, 4, 1, GATHER_MAX><<<G, 256, 0, s>>>(a);
         }
-    } else if (shape == 1) {
-        if (ef) tv16_lscan<true, 8, 4, 0><<<G, 512, 0, s>>>(a);
-        else tv16_lscan<false, 8, 4, 0><<<G, 512, 0, s>>>(a);
     } else {
         if (ef) tv16_lscan<true, 4, 8, 0><<<G, 256, 0, s>>>(a);
         else tv16_lscan<false, 4, 8, 0><<<G, 256, 0, s>>>(a);

@@ -19,7 +19,6 @@ constexpr uint32_t TOPK_LIST_CAP = 4096;     // top-k: keys of T's level-2 bin l
 constexpr uint32_t TOPK_LIST_TILES = 8192;   // ... when the bucket has at most this many tiles (64 Mi floats)
 constexpr uint32_t TV_MAXG = 2048;           // threshold-v ranges (workgroups) per call
 constexpr uint32_t TV_SCAP = 4096;           // threshold-v qualifiers listed per range (32 KiB of LDS)
-constexpr uint32_t TV_MAXNG = 16384;         // threshold-v chunk groups (32 chunks of 32 KiB) per call at most
 
 constexpr uint32_t RS_BINS = 2048;           // radix-select bins (11 bits)
 constexpr uint32_t RS_SHARDS = 8;            // histogram copies: workgroup w adds into shard w % RS_SHARDS
@@ -118,16 +117,12 @@ constexpr uint32_t TK1_LINE = 32;   // words per 128-byte line: every shard coun
 constexpr uint32_t TK2_FINE = 1u << 18;               // band bins: one per ulp
 constexpr uint32_t TK2_CSH = 8;                       // coarse bins: 256 ulps
 constexpr uint32_t TK2_COARSE = TK2_FINE >> TK2_CSH;  // 1024
-#ifndef STG_TK2_CSHARDS
-#define STG_TK2_CSHARDS 1  // 4 and 8 copies measured slower (profiles/r05_topk_finish_ab.jsonl)
-#endif
-constexpr uint32_t TK2_CSHARDS = STG_TK2_CSHARDS;     // copies of the coarse bins (each tile adds into one)
+constexpr uint32_t kTk2Cshards = 1;  // 4 and 8 copies measured slower (profiles/r05_topk_finish_ab.jsonl)
+constexpr uint32_t TK2_CSHARDS = kTk2Cshards;     // copies of the coarse bins (each tile adds into one)
 constexpr uint32_t TK2_HI = 16;                       // shards of the count of keys above the band
 constexpr uint32_t TK2_REG = 32;                      // superset regions (tile mod 32), an offset counter each
-#ifndef STG_TK2_UT
-#define STG_TK2_UT 16
-#endif
-constexpr uint32_t TK2_UT = STG_TK2_UT;               // tiles per emission unit (at most)
+constexpr uint32_t kTk2Ut = 16;
+constexpr uint32_t TK2_UT = kTk2Ut;               // tiles per emission unit (at most)
 constexpr uint32_t TK2_UNITS = TOPK_LIST_TILES / TK2_UT;
 struct alignas(128) TopkCtl {
     // the stream launch's band [F, H): the next call's stream launch zeroes
@@ -151,9 +146,6 @@ struct DevWS {
     FillCtl *ctl;
     TopkCtl *tkctl;      // [2]
     uint32_t *tkfine;    // [2][TK2_FINE] band histograms by call parity, zero between calls
-    uint64_t *tkdesc;    // [TOPK_LIST_TILES] stream tile t: call tag << 32 | superset entries
-    uint32_t *tkdone;    // [2][TK2_UNITS] unit u finished in the stream launch / its tiles all described: = the call tag
-    uint32_t *tvg;       // [2 parities][sum, max][TV_MAXNG] threshold-v chunk-group counts and maxima, + the call's t
     CrewCtl *crew;       // MAX_BATCH slots
     ChunkDesc *desc;     // thresholdv16 chunk descriptors (grown per launch, zeroed)
     CallParams *cp;
@@ -209,7 +201,6 @@ struct Tv16Launch {
     uint32_t epoch;    // per-workspace call counter, 1..2^24-1 (hand-off tags)
     uint32_t max_wg;     // fused-kernel workgroups at most (its share of 2 per CU)
     uint32_t desc_cap;   // ChunkDesc entries at ws.desc
-    hipEvent_t scan_done;  // optional: recorded between the scan and the fill launch
     uint32_t lone_cap;   // chunks the one-bucket lists (ws.ldesc / lq / lw) hold (0: none)
     uint32_t *lone_calls;  // the workspace's one-bucket path calls (host; its parity picks the
                            // window histogram and arrival block, each call zeroing the other copy)
@@ -311,7 +302,6 @@ struct LScanArgs {
     uint32_t *fail, *dbg;
 };
 hipError_t launch_tv16_lscan(LScanArgs &a, int num_cu, hipStream_t s);
-hipError_t launch_lone_noop(uint32_t grid, uint32_t lds, const uint32_t *w, uint32_t *out, hipStream_t s);
 
 struct TvLaunch {
     const float *src;
@@ -328,12 +318,8 @@ struct TvLaunch {
     uint32_t tag;          // call tag (>= 1) of the range descriptors at ws.tile_cnt (2 words per range)
     uint64_t ticket_base;  // ws.tv_ticket's value when this call starts
     uint32_t *grid_out;    // receives the launch's range count (the ticket advances by it)
-    uint32_t *tv_ng;       // [2]: the chunk groups the last call of each parity used (host memory)
-    uint32_t par;          // this call's parity (alternates per call): group sums it accumulates into
 };
 hipError_t launch_tv(const TvLaunch &a, const DevWS &ws, hipStream_t s);
-uint32_t tv_chunks(size_t n);      // threshold-v chunks (32 KiB) of an n-element bucket
-uint32_t tv_list_words(size_t n);  // ... their qualifier lists, in 32-bit words (ws.sums)
 
 struct TopkLaunch {
     const float *src;

@@ -58,41 +58,20 @@ for s in "$@"; do
         c2) step c2 300 python tools/bench_configs.py --only c2 ;;
         prof_topk) step prof_topk 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_topk" -o run -- python3 tools/bench_configs.py --only topk --cpu-seconds 0
             python3 tools/ktrace.py gpurun_out/prof_topk > gpurun_out/prof_topk.txt 2>&1 ;;
-        c5ab)  # world-1 MERGE emission: 1,024-pair tiles (default) against 4,096 (STG_MERGE_WP=16)
-            for W in 16 4 2 1; do
-                STG_MERGE_WP=$W step c5_wp$W 150 python tools/bench_configs.py --only c5 --cpu-seconds 0
-            done ;;
         prof_c5) step prof_c5 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c5" -o run -- python3 tools/bench_configs.py --only c5
             python3 tools/ktrace.py gpurun_out/prof_c5 24 > gpurun_out/prof_c5.txt 2>&1 ;;
         prof_merge) step prof_merge 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_merge" -o run -- python3 tools/bench_configs.py --only merge
             python3 tools/ktrace.py gpurun_out/prof_merge 16 > gpurun_out/prof_merge.txt 2>&1 ;;
         scale_drop) step scale_drop 280 python tools/scale_drop.py 4 ${DROPS:-100,10,2,1.1} ;;
         fill_paths) step fill_paths 200 python tools/fill_paths.py --steps 400 ;;
-        stamps_r4) STG_CODEC_LIB=$R/tools/variants/libstg_codec_tk1st.so step tk1_stamps 150 python tools/tk1_stamps.py
-            STG_CODEC_LIB=$R/tools/variants/libstg_codec_crewst.so step crew_stamps 150 python tools/crew_stamps.py ;;
         tiny) step tiny 120 python tools/tiny_probe.py
-            STG_TV16_CREW_LONE=0 step tiny_nocrew 120 python tools/tiny_probe.py
             STG_DEBUG_TV16_FILL=2 step tiny_literal 120 python tools/tiny_probe.py ;;
         tests_topk1) step tests_topk1 600 python -u -m pytest tests/test_gpu_topk1.py tests/test_gpu_codecs.py tests/test_gpu_configs.py -k "topk or c2 or hint" -v -m gpu --timeout 300 --timeout-method thread ;;
         tests_wide) step tests_wide 600 python -u -m pytest tests/test_gpu_wide.py tests/test_gpu_fill_modes.py -v -s -m gpu --timeout 300 --timeout-method thread ;;
-        c2ab)  # shipped-mode top-k: the ordered six-launch path (STG_TOPK_BK=0) against the unordered three
-            STG_TOPK_BK=0 step c2_ordered 150 python tools/bench_configs.py --only topk --cpu-seconds 0
-            step c2_bk 150 python tools/bench_configs.py --only topk --cpu-seconds 0
-            for L in tools/variants/libstg_codec_bk*.so; do
-                [ -e "$L" ] || continue
-                v=$(basename $L .so); v=${v#libstg_codec_}
-                STG_CODEC_LIB=$R/$L step c2_$v 150 python tools/bench_configs.py --only topk --cpu-seconds 0
-            done ;;
         tests_topk) step tests_topk 400 python -u -m pytest tests/test_gpu_codecs.py tests/test_gpu_configs.py tests/test_gpu_api.py -k "topk or c2" -v -m gpu --timeout 120 --timeout-method thread ;;
         prof_c2) step prof_c2 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c2" -o run -- python3 tools/bench_configs.py --only c2
             python3 tools/ktrace.py gpurun_out/prof_c2 > gpurun_out/prof_c2.txt 2>&1 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
-        tvvar)  # threshold-v variants built by tools/tv_variants.sh: C3 device timing each
-            for L in tools/variants/libstg_codec_tv*.so; do
-                v=$(basename $L .so); v=${v#libstg_codec_}
-                STG_CODEC_LIB=$R/$L step c3_$v 150 python tools/bench_configs.py --only c3dev --calls 64
-                [ -n "${TV_TESTS:-}" ] && STG_CODEC_LIB=$R/$L step tests_tv_$v 300 python -u -m pytest tests/test_gpu_codecs.py -k "thresholdv_parity" -x -q -m gpu --timeout 120 --timeout-method thread
-            done ;;
         tv_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_tvst.so step tv_stamps 150 python tools/tv_stamps.py ;;
         tests_tv) step tests_tv 400 python -u -m pytest tests -k "thresholdv and not thresholdv16 or c3 or tv_" -v -m gpu --timeout 120 --timeout-method thread ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
@@ -104,25 +83,6 @@ for s in "$@"; do
         tests_wire) step tests_wire 600 python -u -m pytest tests/test_gpu_wire_fused.py tests/test_gpu_wire.py -v -m gpu --timeout 120 --timeout-method thread ;;
         prof_apply) step prof_apply 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_apply" -o run \
                 -- python3 tools/bench_configs.py --only apply ;;
-        depths)  # tuning variants built as stellatrain_amd/libstg_codec_d*.so
-            for L in tools/variants/libstg_codec_*.so; do
-                v=$(basename $L .so); v=${v#libstg_codec_}
-                export STG_CODEC_LIB=$R/$L
-                step depth_$v 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-}
-                if [ -n "${DEPTH_STAGES:-}" ]; then
-                    for st in $DEPTH_STAGES; do
-                        export STG_DEBUG_TV16_STAGE=$st
-                        step depth_${v}_s$st 200 python bench.py --steps 50 --warmup 8 --no-cpu-baseline ${BENCH_ARGS:-}
-                        unset STG_DEBUG_TV16_STAGE
-                    done
-                fi
-                unset STG_CODEC_LIB
-            done ;;
-        streams)  # headline stream counts, default admission vs scans one at a time
-            for S in 1 2 3 4; do
-                step streams_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
-                STG_TV16_SERIAL=1 step streams_serial_s$S 200 python bench.py --steps 40 --warmup 8 --no-cpu-baseline --streams $S
-            done ;;
         lone_bench) step lone_bench 200 ./tools/lone_bench 16 96 ;;
         prof_lone_bench) step prof_lone_bench 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lone_bench" -o run -- ./tools/lone_bench 16 96 ;;
         prof_lone)  # kernel durations of the single-caller lone bench (production library)
