@@ -828,7 +828,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         {
             static const uint32_t fill_mode0 =
                 getenv("STG_DEBUG_TV16_FILL") ? (uint32_t)atoi(getenv("STG_DEBUG_TV16_FILL")) : 0u;
-            const bool lf2 = lf2_env != 0 && !fused_gather && !a.b[0].wflag && lf2_fin > lf2_wk;
+            const bool lf2 = lf2_env != 0 && !a.b[0].wflag && lf2_fin > lf2_wk;
             L.fin = lf2 ? lf2_fin : 0u;
             L.nwk = lf2_wk;
             L.mode = fill_mode0;

@@ -111,17 +111,13 @@ struct Lf2Lds {
     float tail[16];
 };
 
-// 16-byte global stores / loads through pointers taken from LDS (an address
-// space the compiler cannot see: without the cast they become flat accesses,
-// which count against lgkmcnt as well as vmcnt)
+// 16-byte global stores through pointers taken from LDS (an address space the
+// compiler cannot see: without the cast they become flat accesses, which count
+// against lgkmcnt as well as vmcnt)
 __device__ __forceinline__ void st_g16(void *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     u4v v;
     v.x = a; v.y = b; v.z = c; v.w = d;
     *(__attribute__((address_space(1))) u4v *)p = v;
-}
-__device__ __forceinline__ float4 ld_g16(const void *p) {
-    const u4v v = *(__attribute__((address_space(1))) const u4v *)p;
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
 }
 
 // 16 bytes at element `i` of `base` (uniform base), sc1
@@ -160,7 +156,8 @@ __device__ __forceinline__ void lf2_decide(Lf2Lds &L, Lf2Dec &D, uint32_t (&h)[4
     constexpr uint32_t RH = LF2_PER / 2;  // loads per thread per round (chunk tid + 256 u)
     uint32_t sw = 0, bad = 0;
     D.ok = true;
-    if (tid < A.tl) L.tail[tid] = *gp(A.src + (size_t)A.nb * 16 + tid);  // (in LDS: thread 0 sums them in order)
+    // (sc1 loads of the bucket: under the fused gather this launch wrote it)
+    if (tid < A.tl) L.tail[tid] = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(A.src) + (size_t)A.nb * 16 + tid));  // (in LDS: thread 0 sums them in order)
     const float t0 = A.t, i0 = A.inc;
     for (uint32_t h0 = 0; h0 * RH * LF2_WG < nc; ++h0) {
         uint64_t x[RH];
@@ -320,10 +317,11 @@ __device__ __forceinline__ bool lf2_worker(Lf2Lds &L, uint32_t wk) {
         const size_t p0 = (size_t)A.nb * 16;
         for (uint32_t i = 0; i < D.ct; ++i) {
             *gp(A.idx + D.c0 + i) = (uint32_t)(p0 + i) + (uint32_t)A.idx_offset;
-            *gp(A.val + D.c0 + i) = *gp(A.src + p0 + i);
+            *gp(A.val + D.c0 + i) = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(A.src) + p0 + i));
         }
         if (A.resid)  // fused error feedback: the ragged tail is not streamed
-            for (uint32_t i = 0; i < A.tl; ++i) *gp(A.resid + p0 + i) = *gp(A.src + p0 + i);
+            for (uint32_t i = 0; i < A.tl; ++i)
+                *gp(A.resid + p0 + i) = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(A.src) + p0 + i));
         auto st = gp(A.state);
         st->t = D.regimeB ? (float)((double)D.t * 0.99) : D.t + D.inc;  // thresholdv16.cpp:243-259
         st->inc = D.inc;
@@ -596,6 +594,7 @@ __device__ __forceinline__ bool lf2_ranker(Lf2Lds &L, uint32_t rk) {
     // ---- the share's pops (ranks [E0, min(E1, P)), four lanes per line):
     //      their loads go out now, the stores wait for the checks ----
     const bool vec = lf2_aligned(A) && (D.cnt & 3u) == 0;
+    const uint32_t src_bytes = A.nb * 64u;  // the full lines (< 2^32 bytes: LMAXC chunks of LCHUNK lines)
     const uint32_t s1 = min(E1, P), q = tid & 3u;
     constexpr uint32_t LPR = LF2_WG / 4, NRD = 2;
     float4 v[NRD];
@@ -611,7 +610,7 @@ __device__ __forceinline__ bool lf2_ranker(Lf2Lds &L, uint32_t rk) {
                 if (off[u] < rem) {
                     len[u] = min(i == tr ? A.tl : 16u, rem - off[u]);
                     pos[u] = L.u.r.kl[L.u.r.ord[i - E0]] * 16u;
-                    if (vec && len[u] == 16 && (off[u] & 3u) == 0) v[u] = ld_g16(A.src + pos[u] + 4 * q);
+                    if (vec && len[u] == 16 && (off[u] & 3u) == 0) v[u] = ld_sc1_f4(reinterpret_cast<const float4 *>(A.src), src_bytes, pos[u] / 4 + q);
                 }
             }
         }
@@ -627,7 +626,10 @@ __device__ __forceinline__ bool lf2_ranker(Lf2Lds &L, uint32_t rk) {
                        __float_as_uint(v[u].w));
             } else {
                 for (uint32_t cc = 0; cc < 4; ++cc)
-                    if (4 * q + cc < len[u]) { *gp(A.idx + o + cc) = bi + cc; *gp(A.val + o + cc) = *gp(A.src + (size_t)pos[u] + 4 * q + cc); }
+                    if (4 * q + cc < len[u]) {
+                        *gp(A.idx + o + cc) = bi + cc;
+                        *gp(A.val + o + cc) = u2f(ld_sc1(reinterpret_cast<const uint32_t *>(A.src) + (size_t)pos[u] + 4 * q + cc));
+                    }
             }
         }
     };

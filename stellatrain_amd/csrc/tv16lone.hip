@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
         const size_t e = (size_t)A.nb * 16 + tid;
         float acc = A.src[e];
         for (uint32_t x = 0; x < ns; ++x) acc += xs(x)[e];
-        const_cast<float *>(A.src)[e] = acc;
+        st_sc1(reinterpret_cast<uint32_t *>(const_cast<float *>(A.src)) + e, f2u(acc));  // (read by the finish: sc1)
     }
     // the next call's counters (the finish of this call uses the other copy)
     if (blockIdx.x == 0 && tid < sizeof(CallCtl) / 4) st_sc1(A.zero_next + tid, 0u);
@@ -214,7 +214,9 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
             asm volatile("" : "+v"(voff));
             u4v t4;
             t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);
-            __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc, voff + m * (NW * 1024u), 0, 0);
+            // written through: the finish in this launch reads popped lines
+            // from the bucket (sc1 loads) once the chunk is listed
+            __builtin_amdgcn_raw_buffer_store_b128(t4, rsrc, voff + m * (NW * 1024u), 0, 16 /* sc1 */);
         };
         auto store_r = [&](uint32_t m, float4 x) {
             uint32_t voff = lane_line * 64u + q * 16u;
@@ -303,13 +305,14 @@ __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(GS
             }
         }
         lds_drain();
+        if (GS) vm_drain();  // the gathered sums stored before the chunk's counts are (the finish reads them)
         uint32_t old = 0;
         if (lane == 0) old = atomicAdd(&L.done[sl], 1u);
         if (uni(old) == NW - 1) {  // every other wave's list adds were drained first
             finalize(L, A, sl, c, j, tb);
         }
     }
-    if (!GS && A.fin && blockIdx.x + A.fin >= gridDim.x)
+    if (A.fin && blockIdx.x + A.fin >= gridDim.x)
         lf2_finish(U.f, A, blockIdx.x + A.fin - gridDim.x, t, inc0);
 }
 
@@ -325,7 +328,7 @@ hipError_t launch_tv16_lscan(LScanArgs &a, int num_cu, hipStream_t s) {
     const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(a.nc, per_cu * (uint32_t)num_cu));
     // the finish's roles: the last `fin` workgroups of the grid, at least
     // nwk + 1 of them (a ranker); else the fill launch finishes the call
-    if (a.fin && (G < 2 * a.fin || a.fin <= a.nwk || a.nwk < 8 || a.nc > LMAXC || a.gn || !a.tag)) a.fin = 0;
+    if (a.fin && (G < 2 * a.fin || a.fin <= a.nwk || a.nwk < 8 || a.nc > LMAXC || !a.tag)) a.fin = 0;
     if (a.gn) {  // the gather fused: fewer loads in flight per stream, more streams
         const uint32_t ns = (a.gres ? 1u : 0u) + a.gn - 1u;
         if (a.gn > GATHER_MAX) return hipErrorInvalidValue;
