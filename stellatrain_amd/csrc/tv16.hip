@@ -819,8 +819,7 @@ hipError_t launch_tv16(const Tv16Launch &a, const DevWS &ws, hipStream_t s) {
         L.tag = tag;
         L.done = ws.larr;
         L.tl = (uint32_t)(a.b[0].n % 16);
-        // the finish inside the scan launch (tv16lf2.h): not under the fused
-        // gather (the scan rewrites the bucket) or the wire form
+        // the finish inside the scan launch (tv16lf2.h): not for the wire form
         static const int lf2_env = getenv("STG_TV16_LF2") ? atoi(getenv("STG_TV16_LF2")) : 1;
         // 48 workers + 16 rankers (profiles/r05_lf2_roles_sweep.txt)
         constexpr uint32_t lf2_fin = 64, lf2_wk = 48;

@@ -57,6 +57,7 @@ constexpr uint32_t LF2_PER = LMAXC / LF2_WG;        // chunks per thread in the 
 constexpr uint32_t LF2_NONE = 0xffffffffu;
 constexpr uint32_t LF2_POS_LIM = (1u << 20) - 1;    // rf_key's 20-bit paths
 constexpr uint32_t LF2_TIES = 1u, LF2_VIOL = 2u;
+constexpr uint32_t LF2_DBG_STALE = 31;            // debug word: workers the freshness check sent to the fill launch (tests read it)
 constexpr uint32_t LF2_RC = 280;                    // a ranker's share of kept entries, at most
 static_assert(LF2_KE * LF2_WG == LF2_WK && LF2_PER * LF2_WG == LMAXC, "per-thread counts");
 static_assert(LNBIN == 4 * LF2_WG, "four bins per thread");
@@ -285,7 +286,8 @@ __device__ __forceinline__ bool lf2_worker(Lf2Lds &L, uint32_t wk) {
     // sub, sub + TPC, ... of the chunk's lines below lim
     const uint32_t gt = wk * LF2_WG + tid, tpc = max(1u, nwk * LF2_WG / nc), c = gt / tpc, sub = gt % tpc;
     const bool vec = lf2_aligned(A);
-    const uint32_t lv_bytes = nc * LQCAP * 4u * 16u;
+    const uint32_t lv_bytes = nc * LQCAP * 4u * 16u, tag16 = A.tag & 0xffffu;
+    uint32_t stale = 0;  // a listed line without this call's tag (tv16lone.hip finalize)
     if (wk == 0) LF2_STAMP(20);
     for (uint32_t cc = c; cc < nc; cc += nwk * LF2_WG / tpc) {  // (one pass unless nc > nwk LF2_WG)
         const uint32_t g0 = L.qp16[cc];
@@ -308,9 +310,21 @@ __device__ __forceinline__ bool lf2_worker(Lf2Lds &L, uint32_t wk) {
 #pragma unroll
             for (uint32_t j = 0; j < K; ++j) {
                 const uint32_t t = t0 + j * tpc;
-                if (t < ne) lf2_store(A, vec, g0 + (t >> 2), D.kb, D.r, cc * LCHUNK + ln[j], x[j], t & 3u);
+                if (t < ne) {
+                    stale |= (ln[j] >> 16) != tag16 ? 1u : 0u;
+                    lf2_store(A, vec, g0 + (t >> 2), D.kb, D.r, cc * LCHUNK + (ln[j] & 0xffffu), x[j], t & 3u);
+                }
             }
         }
+    }
+    // Consistency: every list entry this worker emitted must carry the call's
+    // tag.  One that does not means a list read before its chunk's stores were
+    // visible (or a count pair not from this call): the worker does not count
+    // itself done, and the fill launch, after the kernel boundary, emits the
+    // call again from the same lists.
+    if (__syncthreads_or((int)stale)) {
+        if (tid == 0) g_add(&A.dbg[LF2_DBG_STALE], 1u);
+        return false;
     }
     // worker 0: tail, AIMD state, count (tv16.hip finish_chunk, lfin_worker)
     if (wk == 0 && tid == 0) {

@@ -248,7 +248,7 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
     for (uint32_t i = 0; i < NS; ++i) {
         const uint32_t t = tid + i * FILL_WG, c = c_lo + t / (LF_SPEC * 4), sl = (t / 4) % LF_SPEC;
         if (t < nspec) {
-            ls[i] = A.lq[(size_t)c * LQCAP + sl];
+            ls[i] = A.lq[(size_t)c * LQCAP + sl] & 0xffffu;  // (the call's tag above the line)
             xs[i] = A.lv[((size_t)c * LQCAP + sl) * 4 + (t & 3u)];
         }
     }
@@ -275,7 +275,7 @@ __device__ __noinline__ void lfin_worker(LfinLds &L, uint32_t wk) {
         for (uint32_t t = s0 * 4 + tid; t < qc * 4; t += FILL_WG) {
             const uint32_t sl = t / 4, g = qp[c] + sl;
             if (g >= D.lim) continue;
-            lfin_store(d, vec, g, D.kb, D.r, c * LCHUNK + A.lq[(size_t)c * LQCAP + sl],
+            lfin_store(d, vec, g, D.kb, D.r, c * LCHUNK + (A.lq[(size_t)c * LQCAP + sl] & 0xffffu),
                        A.lv[((size_t)c * LQCAP + sl) * 4 + (t & 3u)], t & 3u);
         }
     }

@@ -14,7 +14,8 @@
 // workgroup ever waits on another: chunk c goes to workgroup c mod G, and
 // each chunk leaves only its lists --
 //   ldesc[c] = {qualifying lines, window lines}       (true counts)
-//   lq[c][r] = the r-th qualifying line of the chunk   (line within the chunk)
+//   lq[c][r] = the r-th qualifying line of the chunk   (line within the chunk;
+//              the call's tag, low 16 bits, above it: the finish's freshness check)
 //   lv[c][r] = its 16 floats (staged from the stream: the finish never re-reads them)
 //   lw[c][r] = {sum bits, line | qualifying lines before it << 16} of its r-th
 //              window line (sum in [t - 2^18 ulps, t), thresholdv16 regime B)
@@ -77,6 +78,7 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
     const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(lq, 0, LQCAP * 4u, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(lv, 0, LQCAP * 64u, 0x00020000);
     const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(A.went, 0, LNBIN * LBCAP * 8u, 0x00020000);
+    const uint32_t qtag = (A.tag ^ (A.skip == 5 ? 1u : 0u)) << 16;  // (STG_LF2_SKIP=5: a wrong tag, the check's test)
     // entry e of the list has rank r_e; its line data (four float4) goes to
     // lv[r_e]: lane = 16 entries x 4 quarters per round
     for (uint32_t e0 = 0; e0 < ql; e0 += 16) {
@@ -85,7 +87,7 @@ __device__ __forceinline__ void finalize(LLds &L, const LScanArgs &A, uint32_t s
             const uint32_t li = L.ql[sl][e];
             uint32_t r = 0;
             for (uint32_t x = 0; x < ql; ++x) r += L.ql[sl][x] < li;
-            if (qq == 0) __builtin_amdgcn_raw_buffer_store_b32(li, rq, r * 4u, 0, 16 /* sc1 */);
+            if (qq == 0) __builtin_amdgcn_raw_buffer_store_b32(li | qtag, rq, r * 4u, 0, 16 /* sc1 */);
             const float4 x = L.qv[sl][e][qq];
             u4v t4;
             t4.x = __float_as_uint(x.x); t4.y = __float_as_uint(x.y); t4.z = __float_as_uint(x.z); t4.w = __float_as_uint(x.w);

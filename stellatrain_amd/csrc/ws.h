@@ -291,7 +291,7 @@ struct LScanArgs {
     // and of the next (zeroed here), and the next call's window histogram
     uint32_t fin, nwk, mode;
     uint32_t tag;          // the call's tag (>= 1) on every chunk's counts
-    uint32_t skip;         // diagnostics (STG_LF2_SKIP): a role stops at that point
+    uint32_t skip;         // diagnostics (STG_LF2_SKIP): a role stops at that point (5: the lists carry a wrong tag)
     uint32_t *done;        // per role: the tag once its part is written (LARR_WORDS)
     uint32_t *whist_next;
     uint32_t *out_idx;

@@ -8,7 +8,9 @@ parent (read once per process: 0 = production, 1 = always the shadow heap,
 the crew), checks every call's whole stream against the oracle, and prints the
 fill's path counters (debug words 56..59: the orderer's ways), the one-bucket
 finish's (48..51: rankers without ties, rankers with ties, the orderer after
-a violation, the orderer for a call the rankers could not take) and the wide
+a violation, the orderer for a call the rankers could not take), the scan
+finish's freshness check (31: workers that found a list entry without the
+call's tag and left the call to the fill launch) and the wide
 paths' (52..55: the orderer's leader, crew buckets, the orderer's leader
 failing to the literal heap, the crew's leader failing to it) as one JSON
 line.
@@ -84,7 +86,7 @@ def main():
     w = (C.c_uint32 * 64)()
     check(lib().stg_codec_debug_words(comp._h, C.c_void_p(st.cuda_stream), w, 64))
     print(json.dumps({"ok": True, "calls": calls, "paths": list(w)[56:60], "lfin": list(w)[48:52],
-                      "scan_ranked": list(w)[44:46],
+                      "scan_ranked": list(w)[44:46], "stale": w[31],
                       "wide": list(w)[52:56], "mode": os.environ.get("STG_DEBUG_TV16_FILL")}), flush=True)
 
 

@@ -44,18 +44,27 @@ def test_production_order(gpu):
     out = _child(0)
     plain, tied, viol, notake = out["lfin"]
     assert out["scan_ranked"][1] > 0, out  # ranked with ties in the scan launch
+    assert out["stale"] == 0, out  # no list entry without its call's tag (tv16lf2.h freshness check)
     assert out["paths"][3] == 0, out  # never the literal heap
     leader, crew, leader_lit, crew_lit = out["wide"]
     assert crew > 0 and leader_lit == 0 and crew_lit == 0, out
 
 
-@pytest.mark.parametrize("env", [{"STG_TV16_LF2": "0"}, {"STG_LF2_SKIP": "1"}, {"STG_LF2_SKIP": "4"}],
-                         ids=["lfin_only", "scan_rankers_give_up", "scan_workers_give_up"])
+@pytest.mark.parametrize("env", [{"STG_TV16_LF2": "0"}, {"STG_LF2_SKIP": "1"}, {"STG_LF2_SKIP": "4"},
+                                 {"STG_LF2_SKIP": "5"}],
+                         ids=["lfin_only", "scan_rankers_give_up", "scan_workers_give_up", "scan_lists_stale"])
 def test_production_order_fill_finish(gpu, env):
     """The fill launch's finish (tv16lfin.h): with the scan's finish off, or
     with its rankers / workers giving up (STG_LF2_SKIP), the fill launch's
-    rankers order the regime-B fills (with ties), bit-exact as before."""
+    rankers order the regime-B fills (with ties), bit-exact as before.  With
+    STG_LF2_SKIP=5 the scan tags its lists with a wrong call tag: the finish's
+    freshness check must send every call with qualifying lines to the fill
+    launch (debug word 31) and the streams stay bit-exact."""
     out = _child(0, **env)
+    if env.get("STG_LF2_SKIP") == "5":
+        assert out["stale"] > 0, out
+    else:
+        assert out["stale"] == 0, out
     plain, tied, viol, notake = out["lfin"]
     assert tied > 0, out
     assert out["paths"][3] == 0, out  # never the literal heap

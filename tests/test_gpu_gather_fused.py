@@ -12,12 +12,21 @@ as its own pass), steady calls (fused), ragged tails, N = 1, 2, 4 and 9, with
 and without the residual."""
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
 from parity import assert_same_stream
 
 pytestmark = pytest.mark.gpu
+
+
+def _words(comp, stream):
+    from stellatrain_amd._capi import check, lib
+    w = (C.c_uint32 * 64)()
+    check(lib().stg_codec_debug_words(comp._h, C.c_void_p(stream.cuda_stream), w, 64))
+    return list(w)
 
 
 def _np_gather(g, resid):
@@ -79,5 +88,9 @@ def test_gather_fused_matches_separate(gpu, oracle, n, N, with_resid):
                 r_np = r_f.cpu().numpy().copy()
         fused.check_device()
         sep.check_device()
+        # the in-scan finish's freshness check (tv16lf2.h) never had to send a
+        # call to the fill launch: every list entry carried its call's tag
+        st = torch.cuda.current_stream()
+        assert _words(fused, st)[31] == 0 and _words(sep, st)[31] == 0
     finally:
         oracle.tv16_free(ho)

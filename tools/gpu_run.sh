@@ -72,13 +72,13 @@ for s in "$@"; do
         prof_c2) step prof_c2 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_c2" -o run -- python3 tools/bench_configs.py --only c2
             python3 tools/ktrace.py gpurun_out/prof_c2 > gpurun_out/prof_c2.txt 2>&1 ;;
         c3) step c3 300 python tools/bench_configs.py --only c3 ;;
-        tv_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_tvst.so step tv_stamps 150 python tools/tv_stamps.py ;;
         tests_tv) step tests_tv 400 python -u -m pytest tests -k "thresholdv and not thresholdv16 or c3 or tv_" -v -m gpu --timeout 120 --timeout-method thread ;;
         c4) step c4 300 python tools/bench_configs.py --only c4 ;;
         c5) step c5 300 python tools/bench_configs.py --only c5 ;;
         apply) step apply 300 python tools/bench_configs.py --only c5,apply ;;
         ef) step ef 300 python tools/bench_configs.py --only ef ;;
         gather) step gather 300 python tools/bench_configs.py --only gather ;;
+        gfused) step gfused 300 python tools/bench_configs.py --only gfused,single ;;
         wfused) step wfused 300 python tools/bench_configs.py --only wfused ;;
         tests_wire) step tests_wire 600 python -u -m pytest tests/test_gpu_wire_fused.py tests/test_gpu_wire.py -v -m gpu --timeout 120 --timeout-method thread ;;
         prof_apply) step prof_apply 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_apply" -o run \
@@ -89,10 +89,6 @@ for s in "$@"; do
             step prof_lone 200 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/prof_lone" -o run -- ./tools/lone_bench 0 96
             python3 tools/ktrace.py gpurun_out/prof_lone 12 > gpurun_out/prof_lone.txt 2>&1 ;;
         lfin_probe) step lfin_probe 200 python tools/lfin_probe.py ;;
-        prof_lfin_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_stamps.so step prof_lfin_stamps 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_lfin_stamps" -o run -- python3 tools/lfin_probe.py ;;
-        lfin_stamps) STG_CODEC_LIB=$R/tools/variants/libstg_codec_stamps.so step lfin_stamps 200 python tools/lfin_probe.py ;;
-        fill_stamps) FS_BUCKETS=16 FS_PARITY=1 STG_CODEC_LIB=$R/tools/variants/libstg_codec_stamps.so \
-                step fill_stamps 200 python tools/fill_stamps.py ;;
         *) echo "unknown step $s" >> gpurun_out/summary.txt ;;
     esac
 done
