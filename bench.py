@@ -2,23 +2,26 @@
 """bench.py -- grad-codec GB/s (dense fp32 in), thresholdv16 k=1%.
 
 N = 1 (the headline, BASELINE.json metric on configs[1]'s bucket size): one
-*step* compresses the 16 gradient buckets of one iteration with thresholdv16:
-16 keys ("<layer>@weight") x 64 MiB fp32 (n = 16,777,216, dst_len = 167,772 =
-merge_numel(n, 0.99)), device resident.  The engine issues its MERGE-compress
-tasks from several pool workers at once (engine/modules/compress.cpp:141,
-config.h:7); here the step is four batched C-ABI calls
-(stg_codec_compress_batch_device) of 4 buckets each on four streams = four
-concurrent persistent launches, so one launch's tail and regime-B heap fill
-overlap the others' streaming.  Each rank holds 8 buffer sets of its 16
-buckets (8 GiB, >> the 256 MB Infinity Cache; --sets): step s compresses set
+*step* compresses the 64 gradient buckets of one iteration with thresholdv16:
+64 keys ("<layer>@weight") x 64 MiB fp32 (n = 16,777,216, dst_len = 167,772 =
+merge_numel(n, 0.99)), device resident -- 4 GiB, the fp32 gradient of a
+1-billion-parameter model.  The engine issues its MERGE-compress tasks from
+several pool workers at once (engine/modules/compress.cpp:141, config.h:7);
+here the step is sixteen batched C-ABI calls (stg_codec_compress_batch_device)
+of 4 buckets each, call j on stream j % 4 = four concurrent persistent
+launches, so one launch's tail and regime-B heap fill overlap the others'
+streaming.  (A timed region of K steps carries a fixed start and drain of
+~0.1 ms: at the driver's K = 20, a 16-key step lost ~3 % to it, a 64-key step
+~0.5 %; profiles/r06_keys_per_step_ab.txt.)  Each rank holds 8 buffer sets of
+its buckets (32 GiB, >> the 256 MB Infinity Cache; --sets): step s compresses set
 s % 8, so every key sees a fresh bucket on every step (the engine
 alternates two shm buffers per layer, core.cpp:967, whose contents are fresh
 each iteration) and its AIMD threshold runs its real regime A/B sequence.
 ``--jitter J`` scales each bucket by a seeded factor in [1 - J, 1 + J], so
 that AIMD window misses happen at a gradient-noise rate.  Keys are initialised
-(first-threshold call) before the warmup.  value = 16 x 64 MiB x steps / time.
+(first-threshold call) before the warmup.  value = 64 x 64 MiB x steps / time.
 
-N > 1: the same step on every rank (each its own 16 keys and buckets, seeded
+N > 1: the same step on every rank (each its own 64 keys and buckets, seeded
 by rank): buckets are independent (core.cpp:1052-1087), so the path shards
 with no collective; "scaling": "weak", value = all ranks' bytes / the slowest
 rank's time, and per_rank_GBps lists each rank's rate.
@@ -72,7 +75,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--mib", type=int, default=64)
     p.add_argument("--ratio", type=float, default=0.99)
-    p.add_argument("--keys", type=int, default=16)
+    p.add_argument("--keys", type=int, default=64)
+    p.add_argument("--per-launch", type=int, default=4,
+                   help="headline: buckets per batched call; call j runs on stream j %% S")
     p.add_argument("--method", default="thresholdv16")
     p.add_argument("--workload", choices=["auto", "headline", "c4"], default="auto",
                    help="the main line's workload (auto: the 64 MiB headline at every N; c4: the C4 stream)")
@@ -91,7 +96,7 @@ def parse():
                         "share the chip")
     p.add_argument("--sets", type=int, default=8,
                    help="buffer sets rotated over the steps: each key sees a fresh bucket on every step for "
-                        "SETS steps running (SURVEY 8(d)); 8 x 16 x 64 MiB = 8 GiB per GPU")
+                        "SETS steps running (SURVEY 8(d)); 8 x 64 x 64 MiB = 32 GiB per GPU")
     p.add_argument("--jitter", type=float, default=0.0,
                    help="scale each (key, set) bucket by a seeded factor in [1 - J, 1 + J] (gradient-scale "
                         "noise: AIMD window misses at a realistic rate)")
@@ -221,9 +226,12 @@ def workload(args, world, rank):
     if wl == "headline":
         n = args.mib * (1 << 20) // 4
         ids = list(range(args.keys))
-        items = [(f"{rank * 64 + i}@weight", n, merge_numel(n, args.ratio, 1), rank * 64 + i) for i in ids]
+        span = max(64, args.keys)  # (bucket ids, hence seeds, distinct over the ranks)
+        items = [(f"{rank * span + i}@weight", n, merge_numel(n, args.ratio, 1), rank * span + i) for i in ids]
+        pl = max(1, min(16, args.per_launch))
         desc = {"workload": f"{args.method} k={merge_numel(n, args.ratio, 1)} (1%) on {args.mib} MiB fp32 buckets; "
-                            f"step = one batched call over {args.keys} keys ({args.keys * args.mib} MiB) per GPU",
+                            f"step = {args.keys} keys ({args.keys * args.mib} MiB) per GPU in "
+                            f"{(args.keys + pl - 1) // pl} batched calls of {pl}, call j on stream j % {args.streams}",
                 "n": n, "dst_len": merge_numel(n, args.ratio, 1)}
         return wl, items, desc, {"all": [[b for *_, b in items]]}
     sizes = c4_sizes(args.c4_count, args.c4_lo, args.c4_hi)
@@ -381,7 +389,8 @@ def main():
     # per-step arguments resolved once: batches of <= 16 buckets (headline: the
     # keys split evenly over the streams), batch j on stream j % S
     if wl == "headline":
-        groups = [list(range(j, nb, ns)) for j in range(ns)]
+        pl = max(1, min(16, args.per_launch))
+        groups = [list(range(j, min(j + pl, nb))) for j in range(0, nb, pl)]
     else:
         groups = [list(range(j, min(j + 16, nb))) for j in range(0, nb, 16)]
     plans = []
