@@ -66,7 +66,6 @@ constexpr uint32_t kTv16WlB = 64;
 constexpr uint32_t STAGE_B = kTv16StageB;  // qualifying lines staged in LDS per slot (~20 expected at 1%)
 constexpr uint32_t WL_B = kTv16WlB;  // window candidates listed in LDS per slot
 constexpr uint32_t kTv16PollSleep = 8;  // s_sleep units (64 clocks) between prefix polls
-constexpr uint32_t kTv16Prio = 1;
 constexpr uint32_t GB = 512;        // chunk descriptors gathered per round trip (a 64 MiB bucket has 512)
 // float4 loads in flight per streaming wave: 2 x 14 x 64 x 16 B x SCAN_D per CU
 // (SCAN_D = 3: 84 KiB per CU, just over the ~72 KiB that hides an HBM miss;
@@ -671,7 +670,7 @@ tv16_batch(BatchArgs A) {
             scan_chunk<STAGE, EF, LONE ? SCAN_D_LONE : SCAN_D_BATCH>(C, j, k, wave);
         }
     } else if (wave == FIN) {
-        if (kTv16Prio) __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
+        __builtin_amdgcn_s_setprio(3);  // short bursts issue ahead of the streaming waves
         for (uint32_t j = 0;; ++j) {
             uint64_t st9 = 0;
             for (uint32_t spins = 0; lds_ld(&L.cok[j % CIDR]) != j + 1; ++spins) {

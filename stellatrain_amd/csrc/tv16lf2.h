@@ -140,15 +140,12 @@ constexpr uint32_t kLf2PollSleep = 2;  // s_sleep between the finishers' descrip
 // (MI355X guide, "Valid forms", Consumer).  The lists are stored sc1 and
 // loaded sc1, which the guide's table validates in place of the acquire only
 // at one workgroup per CU; the scan runs eight per CU, so the acquire stays.
-constexpr uint32_t kLf2Acq = 1;
 __device__ __forceinline__ void lf2_acquire() {
-    if (kLf2Acq) {
-        if (threadIdx.x < 64) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
+    if (threadIdx.x < 64) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __syncthreads();
 }
 template <bool WH>
 __device__ __forceinline__ void lf2_decide(Lf2Lds &L, Lf2Dec &D, uint32_t (&h)[4]) {
