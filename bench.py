@@ -29,7 +29,7 @@ rank's time, and per_rank_GBps lists each rank's rate.
 Every N also carries a ``c4`` sub-object (BASELINE.json configs[3]): the
 1,024-bucket stream (256 KiB - 64 MiB, log-uniform, seeded: shard.c4_sizes)
 sharded over the N ranks by shard.ShardPlan (key-affine, bytes-balanced), one
-sweep = every bucket once in batched launches of <= 16 on four streams; the
+sweep = every bucket once in batched launches of <= 32 on four streams; the
 list is fixed, so that is strong scaling (N = 1 runs the whole stream on one
 GPU).  RCCL carries only the timing barriers and the max / sum reductions.
 
@@ -85,6 +85,8 @@ def parse():
     p.add_argument("--c4-count", type=int, default=1024)
     p.add_argument("--c4-lo", type=int, default=65536)
     p.add_argument("--c4-hi", type=int, default=16777216)
+    p.add_argument("--c4-per-launch", type=int, default=32,
+                   help="c4: buckets per batched call (MAX_BATCH = 32; profiles/r06_c4_per_launch_sweep.txt)")
     p.add_argument("--backend", choices=["hip", "oracle"], default="hip")
     p.add_argument("--dump-shards", default="", help="rank 0 writes every rank's bucket ids here (tests)")
     p.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -228,7 +230,7 @@ def workload(args, world, rank):
         ids = list(range(args.keys))
         span = max(64, args.keys)  # (bucket ids, hence seeds, distinct over the ranks)
         items = [(f"{rank * span + i}@weight", n, merge_numel(n, args.ratio, 1), rank * span + i) for i in ids]
-        pl = max(1, min(16, args.per_launch))
+        pl = max(1, min(32, args.per_launch))
         desc = {"workload": f"{args.method} k={merge_numel(n, args.ratio, 1)} (1%) on {args.mib} MiB fp32 buckets; "
                             f"step = {args.keys} keys ({args.keys * args.mib} MiB) per GPU in "
                             f"{(args.keys + pl - 1) // pl} batched calls of {pl}, call j on stream j % {args.streams}",
@@ -247,7 +249,7 @@ def workload(args, world, rank):
 
 def c4_measure(args, world, rank, comp, streams, dist):
     """The c4 sub-object: this rank's ShardPlan share of the C4 stream, two
-    buffer sets, one sweep = every bucket once (batches of <= 16 distinct keys,
+    buffer sets, one sweep = every bucket once (batches of <= 32 distinct keys,
     batch j on stream j % S); max over ranks of the timed sweeps."""
     import ctypes as C
 
@@ -273,7 +275,8 @@ def c4_measure(args, world, rank, comp, streams, dist):
     oidx = torch.zeros(max(sum(ks), 1), dtype=torch.int32, device=dev)
     oval = torch.zeros(max(sum(ks), 1), dtype=torch.float32, device=dev)
     counts = torch.zeros(max(len(mine), 1), dtype=torch.int32, device=dev)
-    groups = [list(range(j, min(j + 16, len(mine)))) for j in range(0, len(mine), 16)]
+    cpl = max(1, min(32, args.c4_per_launch))
+    groups = [list(range(j, min(j + cpl, len(mine)))) for j in range(0, len(mine), cpl)]
     plans = []
     for par in range(2):
         calls = []
@@ -386,13 +389,13 @@ def main():
     oval = torch.zeros(max(sum(ks), 1), dtype=torch.float32, device=dev)
     counts = torch.zeros(max(nb, 1), dtype=torch.int32, device=dev)
 
-    # per-step arguments resolved once: batches of <= 16 buckets (headline: the
-    # keys split evenly over the streams), batch j on stream j % S
+    # per-step arguments resolved once: batches of --per-launch buckets (headline)
+    # or of 32 (c4 as the main line), batch j on stream j % S
     if wl == "headline":
-        pl = max(1, min(16, args.per_launch))
+        pl = max(1, min(32, args.per_launch))
         groups = [list(range(j, min(j + pl, nb))) for j in range(0, nb, pl)]
     else:
-        groups = [list(range(j, min(j + 16, nb))) for j in range(0, nb, 16)]
+        groups = [list(range(j, min(j + 32, nb))) for j in range(0, nb, 32)]
     plans = []
     for par in range(nsets):
         calls = []

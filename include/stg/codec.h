@@ -94,7 +94,7 @@ typedef struct stg_bucket {
  * on buckets[0..nbuckets-1] in order on `stream`.  It stands in for the
  * engine's concurrent MERGE-compress tasks of one iteration (ThreadPool
  * workers calling compress() on different keys, engine/modules/compress.cpp:
- * 141, engine/config.h:7).  thresholdv16 runs up to 16 buckets with distinct
+ * 141, engine/config.h:7).  thresholdv16 runs up to 32 buckets with distinct
  * keys in one persistent launch, overlapping bucket b's count exchange with
  * bucket b+1's streaming pass; a repeated key starts a new launch. */
 int stg_codec_compress_batch_device(stg_codec_t h, const stg_bucket_t *buckets, size_t nbuckets, void *stream);

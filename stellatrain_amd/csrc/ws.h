@@ -30,7 +30,7 @@ constexpr uint32_t RS_SH_HIST = 4;           // ... of which rs_hist's one workg
 // other copy for the next call (the next call on this workspace is
 // stream-ordered after this launch).  Words handed between workgroups carry
 // the call tag (epoch << 8 | kind) so stale words of earlier calls never match.
-constexpr uint32_t MAX_BATCH = 16;
+constexpr uint32_t MAX_BATCH = 32;
 constexpr uint32_t TV16_CHUNK = 2048;        // lines (16 floats) per chunk = 128 KiB
 struct CallCtl {
     uint32_t next;      // dynamic chunk counter

@@ -268,15 +268,15 @@ BATCH = [
 ]
 
 
-@pytest.mark.parametrize("layout", ["mixed", "sixteen", "short_chunks"])
+@pytest.mark.parametrize("layout", ["mixed", "full_batch", "short_chunks"])
 def test_thresholdv16_batch(gpu, oracle, layout):
     import torch
     from stellatrain_amd import ThresholdvCompressor16
     iters = 7
     if layout == "mixed":
         spec = BATCH
-    elif layout == "sixteen":  # a full batch of 16 distinct keys, then one more (17 -> two launches)
-        spec = [(f"s{i}@w", 131072 + 16 * i + (i % 3), 1311 + i, D1 if i % 2 else D2, 0) for i in range(17)]
+    elif layout == "full_batch":  # a full batch of 32 distinct keys (MAX_BATCH), then one more: two launches
+        spec = [(f"s{i}@w", 131072 + 16 * i + (i % 3), 1311 + i, D1 if i % 2 else D2, 0) for i in range(33)]
     else:
         # more chunks than two per workgroup (dynamic chunk takes) and every
         # bucket ending in a short chunk: streaming waves with no lines there

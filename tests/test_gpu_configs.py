@@ -168,9 +168,9 @@ def test_c4_stream_1024_buckets(gpu):
         for b, n in enumerate(sizes):
             fill(flat[offs[b]:offs[b + 1]], seed_for(b, sw))
         counts = torch.zeros(len(sizes), dtype=torch.int32, device=gpu)
-        for j in range(0, len(sizes), 16):  # batched launches of 16 distinct keys
+        for j in range(0, len(sizes), 32):  # batched launches of 32 distinct keys (MAX_BATCH)
             items = [(plan.key(b), flat[offs[b]:offs[b + 1]], ks[b], oidx[koffs[b]:koffs[b + 1]],
-                      oval[koffs[b]:koffs[b + 1]]) for b in range(j, min(j + 16, len(sizes)))]
+                      oval[koffs[b]:koffs[b + 1]]) for b in range(j, min(j + 32, len(sizes)))]
             comp.compress_batch_async(items, counts=counts[j:])
         torch.cuda.synchronize()
         cn, ih, vh = counts.cpu().numpy(), oidx.cpu().numpy().view(np.uint32), oval.cpu().numpy()
