@@ -12,7 +12,7 @@ times the other configs on one GPU and prints one JSON line per measurement:
       serial (stg_codec_compress_host) and with the H2D of bucket i+1
       overlapped with the codec on bucket i (two streams);
   C4  the 1024-bucket stream (256 KiB..64 MiB, log-uniform, seeded) through
-      thresholdv16 batches of 16, device resident;
+      thresholdv16 batches of 32, device resident;
   C5  compress -> MERGE decompress -> sparse SGD (momentum 0.9) on 64 MiB,
       and the same with sparse Adam (plain and amsgrad) as the apply;
   APPLY  the optimizer applies alone on a 64 MiB param (k = 167,772 pairs
@@ -209,8 +209,8 @@ def c4_stream(torch, batches_timed, streams=1):
     comp = ThresholdvCompressor16()
     rows = [(plan.key(i).encode(), flat[offs[i]:].data_ptr(), sizes[i], ks[i], oidx[koffs[i]:].data_ptr(), ks[i],
              oval[koffs[i]:].data_ptr(), counts.data_ptr() + 4 * i) for i in ids]
-    batches = [comp.bucket_array(rows[j:j + 16]) for j in range(0, len(rows), 16)]
-    nrows = [len(rows[j:j + 16]) for j in range(0, len(rows), 16)]
+    batches = [comp.bucket_array(rows[j:j + 32]) for j in range(0, len(rows), 32)]  # (MAX_BATCH)
+    nrows = [len(rows[j:j + 32]) for j in range(0, len(rows), 32)]
 
     # batch j on stream j % S (keys are distinct within a sweep, so batches are
     # independent; a key's next batch is a sweep later, stream-ordered after
