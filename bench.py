@@ -527,7 +527,10 @@ def main():
                          "basis": "step-level: algorithmic bytes of the profiled steps over their chip interval "
                                   "(HIP events on stream 0, the other streams joined); the per-launch kernel "
                                   "durations overlap (concurrent_launches in flight), so a per-kernel figure "
-                                  "cannot reproduce this frac"},
+                                  "cannot reproduce this frac",
+                         # the same algorithmic bytes over the timed region's wall clock (the clock
+                         # `value` uses, barriers and the last launches' drain included), per GPU
+                         "frac_timed_region": round(alg_step * args.steps / el / 1e9 / HBM_PEAK_GBS, 4)},
             "per_gpu_GBps": round(value / world, 2),
             "per_rank_GBps": per_rank_gbps,
             "rccl_world_size": dist.get_world_size() if world > 1 else 1,
