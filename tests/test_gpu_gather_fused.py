@@ -13,6 +13,9 @@ and without the residual."""
 from __future__ import annotations
 
 import ctypes as C
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -88,9 +91,28 @@ def test_gather_fused_matches_separate(gpu, oracle, n, N, with_resid):
                 r_np = r_f.cpu().numpy().copy()
         fused.check_device()
         sep.check_device()
-        # the in-scan finish's freshness check (tv16lf2.h) never had to send a
-        # call to the fill launch: every list entry carried its call's tag
+        # the in-scan finish's freshness check (tv16lf2.h): in production it never
+        # has to send a call to the fill launch (every list entry carries its
+        # call's tag); with STG_LF2_SKIP=5 the scan tags its lists wrongly and
+        # every call with qualifying lines must go there, bit-exact all the same
         st = torch.cuda.current_stream()
-        assert _words(fused, st)[31] == 0 and _words(sep, st)[31] == 0
+        if os.environ.get("STG_LF2_SKIP") == "5":
+            assert _words(fused, st)[31] > 0 and _words(sep, st)[31] > 0
+        else:
+            assert _words(fused, st)[31] == 0 and _words(sep, st)[31] == 0
     finally:
         oracle.tv16_free(ho)
+
+
+@pytest.mark.skipif(os.environ.get("STG_LF2_SKIP") == "5", reason="already the wrong-tag run")
+def test_gather_fused_wrong_tag_lists_fall_back(gpu):
+    """The four cases above in a child process whose scans tag their lists with
+    a wrong call tag (STG_LF2_SKIP=5, read once per process): the finish's
+    freshness check must hand every call to the fill launch, and every stream
+    must still match the oracle and the separate calls."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, STG_LF2_SKIP="5")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.join(here, "test_gpu_gather_fused.py"), "-q", "-m", "gpu",
+                        "-k", "matches_separate", "-p", "no:cacheprovider"],
+                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
