@@ -218,3 +218,21 @@ def test_topk_argument_copy_names_every_field():
     assert len(fields) > 20, fields
     missing = [f for f in fields if f"A.{f} = Ak.{f};" not in src]
     assert not missing, missing
+
+
+def test_runtime_switches_are_the_documented_ones():
+    """Every STG_* environment switch the library reads is listed in
+    INTEGRATION.md section 4, and the list names no switch the library no
+    longer reads (round 5's verdict: configuration sprawl)."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    read = set()
+    for f in glob.glob(os.path.join(root, "stellatrain_amd", "csrc", "*")):
+        if f.endswith((".hip", ".h", ".cpp")):
+            read |= set(re.findall(r'getenv\("(STG_[A-Z0-9_]+)"\)', open(f).read()))
+    text = open(os.path.join(root, "INTEGRATION.md")).read()
+    para = text[text.index("The runtime switches the library reads are"):]
+    para = para[:para.index("\n\n")]
+    listed = set(re.findall(r"`(STG_[A-Z0-9_]+)", para))
+    assert read == listed, (sorted(read - listed), sorted(listed - read))
